@@ -1,0 +1,39 @@
+# Build: libsimplex.so (gfx950 kernels + C-ABI), the ./solver CLI, and the
+# CPU oracle (test infrastructure).  `make -j8`.  Outputs stay in-tree (git-ignored,
+# shipped to the GPU box with the snapshot).
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+ARCH      ?= gfx950
+PKG       := simplex_method_gpu_amd
+SRC       := $(PKG)/csrc
+BUILD     := $(PKG)/_build
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude
+LDFLAGS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl
+
+LIB       := $(PKG)/libsimplex.so
+CLI       := solver
+
+all: $(LIB) $(CLI) oracle
+
+$(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_device.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/spx_api.o: $(SRC)/spx_api.cpp $(SRC)/spx_kernels.h $(SRC)/spx_device.h include/simplex.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/spx_kernels.o $(BUILD)/spx_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDFLAGS)
+
+$(CLI): $(SRC)/solver_main.cpp include/simplex.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG) -Wl,-rpath,'$$ORIGIN/$(PKG)' -lsimplex
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(CLI)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

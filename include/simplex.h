@@ -1,0 +1,164 @@
+/*
+ * simplex.h — C-ABI of libsimplex, the MI355X (gfx950) dense revised-simplex
+ * hot loop.  Plain pointers and sizes only; no HIP, torch or C++ types.
+ *
+ * What it replaces in the reference (Girjoaba/simplex_method_gpu):
+ *   spx_create + spx_solve + spx_destroy
+ *        <- std::pair<real,SolveStatus> solve(real* A, real* b, real* c,
+ *              real* x_b, int* b_ixs, int m, int n, TimeStruct&)
+ *              src/v4_cub_reduction.cu:219-380 (host buffers in, x_b/b_ixs out)
+ *   spx_price   <- pricing Sgemm + entering ArgMin + optimality test
+ *              src/v4_cub_reduction.cu:288-302
+ *   spx_pivot   <- FTRAN Sgemv, compute_theta, leaving ArgMin, E_q, Sger,
+ *              basis bookkeeping, x_b and y updates
+ *              src/v4_cub_reduction.cu:306-357 (kernels :195-215)
+ *   status codes <- enum class SolveStatus, src/v4_cub_reduction.cu:49-54
+ * The `./solver <file>` CLI built on top of this header replaces main()
+ * (src/v4_cub_reduction.cu:384-473).
+ *
+ * Conventions
+ *   - A is m x n COLUMN-major (column j at A + j*m), as the reference's R2C
+ *     (src/v4_cub_reduction.cu:59-60); the last m columns must be the slack
+ *     identity and b >= 0 (the reference's unchecked assumption, v4:272-277).
+ *   - Everything is fp64.  Indices are 0-based int64.
+ *   - Every function returns SPX_OK (0) or a negative SPX_ERR_* code; nothing
+ *     exits or throws across the ABI.  spx_last_error() gives a message.
+ *   - The caller owns host buffers; the context owns device memory.  One
+ *     context per host thread; a context is not re-entrant.
+ *   - Multi-GPU: one process per GPU.  Pricing columns are sharded over
+ *     opts.nranks ranks (structural and slack columns each split in
+ *     contiguous blocks); B^-1, x_b, y are replicated.  After spx_create,
+ *     every rank calls spx_attach_comm with the id rank 0 obtained from
+ *     spx_comm_unique_id (exchange it out of band, e.g. torch.distributed).
+ */
+#ifndef SIMPLEX_MI355X_H
+#define SIMPLEX_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPX_ABI_VERSION 1
+
+/* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
+#define SPX_STATUS_MAX_ITER       0
+#define SPX_STATUS_OPTIMUM_FOUND  1
+#define SPX_STATUS_UNBOUNDED      2
+#define SPX_STATUS_THETA_OVERFLOW 3 /* kept for ABI parity; unreachable since v2 */
+
+#define SPX_OK             0
+#define SPX_ERR_ARG       -1  /* bad argument (m > n, m <= 0, NULL, ...)     */
+#define SPX_ERR_HIP       -2  /* a HIP runtime call failed                     */
+#define SPX_ERR_OOM       -3  /* device allocation failed                      */
+#define SPX_ERR_RCCL      -4  /* an RCCL call failed                           */
+#define SPX_ERR_STATE     -5  /* call not valid in the context's state         */
+#define SPX_ERR_NO_DEVICE -6  /* no HIP device visible                         */
+
+typedef struct spx_ctx spx_ctx;
+
+typedef struct spx_opts {
+    double  eps;          /* optimality tolerance on reduced costs: optimum when
+                             min_j e_j >= -eps (reference EPS, v4:18: 1e-4 f32);
+                             default 1e-7 (fp64)                */
+    int32_t device;       /* HIP device ordinal; -1 = keep the current device  */
+    int32_t rank;         /* pricing shard of this process (default 0)         */
+    int32_t nranks;       /* number of shards (default 1)                      */
+    int32_t graph_batch;  /* iterations per captured hipGraph; 0 = auto,
+                             -1 = eager launches                               */
+    int32_t price_block;  /* tuning: threads per pricing workgroup, 0 = auto   */
+    int32_t update_rows;  /* tuning: B^-1 rows per wave in the update, 0 = auto */
+    int32_t price_grid;   /* tuning: pricing workgroups, 0 = auto              */
+    int32_t flags;        /* SPX_FLAG_* bits                                   */
+    int32_t reserved[6];
+} spx_opts;
+
+#define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times) */
+
+void spx_default_opts(spx_opts* opts);
+
+/* Allocate device state, upload A (column-major, ld = m), b, c and set the
+ * slack basis (B^-1 = I, x_b = b, y = c_B; v4:268-280). */
+int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A_colmajor,
+               const double* b, const double* c, const spx_opts* opts);
+
+/* Same, but A, b, c are produced on the device by the seeded generator of
+ * SURVEY.md §8(d) (bit-identical to oracle/simplex_oracle.c orc_generate). */
+int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed,
+                         const spx_opts* opts);
+
+void spx_destroy(spx_ctx* ctx);
+
+/* RCCL plumbing for opts.nranks > 1 (no-ops returning SPX_OK when nranks == 1). */
+#define SPX_COMM_ID_BYTES 128
+int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]);
+int spx_attach_comm(spx_ctx* ctx, const uint8_t id[SPX_COMM_ID_BYTES]);
+
+/* Back to the slack basis (keeps A, b, c). */
+int spx_reset(spx_ctx* ctx);
+
+/* Whole solve, device-resident: at most max_iter loop passes (reference
+ * MAX_ITER, v4:19, do/while at v4:286-359).  Writes z, x_b[m], b_ixs[m] (basis
+ * order) for every status (the reference writes them only on optimum);
+ * pivots = pivots made (the reference's loop counter).  Any output may be
+ * NULL.  Continues from the current basis (call spx_reset to restart). */
+int spx_solve(spx_ctx* ctx, int64_t max_iter, double* z, int64_t* b_ixs,
+              double* x_b, int32_t* status, int64_t* pivots);
+
+/* Run up to k further pivots with no host synchronisation between them; one
+ * sync at the end.  status: SPX_STATUS_MAX_ITER while the loop can go on. */
+int spx_iterate(spx_ctx* ctx, int64_t k, int32_t* status, int64_t* pivots);
+
+/* Step-wise API (tests/debugging; each call synchronises).
+ * spx_price: pricing + entering argmin (+ cross-rank MINLOC).  p = entering
+ *   column (first index on ties), min_e = its reduced cost, optimal = 1 when
+ *   min_e >= -eps.
+ * spx_pivot: apply the pending rank-1 update of B^-1 fused with FTRAN
+ *   (alpha = B^-1 A_p), ratio test + leaving argmin, E_q, x_b, y, c_B, basis
+ *   bookkeeping.  Requires a preceding spx_price.  status after the pivot. */
+int spx_price(spx_ctx* ctx, int64_t* p, double* min_e, int32_t* optimal);
+int spx_pivot(spx_ctx* ctx, int64_t* q, int32_t* status);
+
+/* Current state (any pointer may be NULL).  binv_rowmajor: m*m, B^-1[i][k] at
+ * i*m + k (with the pending rank-1 update applied). */
+int spx_get_state(spx_ctx* ctx, double* x_b, int64_t* b_ixs, double* y,
+                  double* c_b, double* binv_rowmajor, int32_t* status,
+                  int64_t* pivots);
+
+/* Reduced costs e_j = -c_j + y.A_j for all n columns from the current y
+ * (debug/parity; basic columns included, like v4:288-290). */
+int spx_reduced_costs(spx_ctx* ctx, double* e);
+
+/* Objective z = c_B . x_b (v4:365), computed on the device. */
+int spx_objective(spx_ctx* ctx, double* z);
+
+/* With SPX_FLAG_TIMING: total device milliseconds and launch counts of the
+ * pricing kernel and of the fused update kernel since the last call (resets). */
+int spx_kernel_times(spx_ctx* ctx, double* price_ms, int64_t* price_launches,
+                     double* update_ms, int64_t* update_launches);
+
+/* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this
+ * rank (8*(m+1)*local non-basic columns), bytes_update: one update launch
+ * (16*m*m), as SURVEY.md §8(d). */
+int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
+             int64_t* local_nonbasic, double* bytes_price, double* bytes_update);
+
+/* Host-only helpers (no device needed), shared with the device code:
+ * spx_shard_range: this rank's column shard — structural columns
+ *   [out[0], out[1]) and slack columns [out[2], out[3]) (global indices).
+ * spx_minloc_merge: the cross-rank MINLOC rule applied to the all-gathered
+ *   candidates — smallest value, then smallest global index (CUB ArgMin's
+ *   first-index semantics, v4:294). */
+int spx_shard_range(int64_t m, int64_t n, int32_t rank, int32_t nranks, int64_t out[4]);
+int spx_minloc_merge(const double* vals, const int64_t* idx, int32_t count,
+                     double* best_val, int64_t* best_idx);
+
+const char* spx_last_error(void);
+const char* spx_status_string(int32_t status);
+int spx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,218 @@
+"""simplex_method_gpu_amd — MI355X-native dense revised-simplex hot loop.
+
+Python mirror of the reference's host interface (Girjoaba/simplex_method_gpu,
+``src/v4_cub_reduction.cu``):
+
+* :func:`read_lp`   <- main()'s LP text reader (v4:395-419, load_matrix v4:94-104)
+* :func:`solve`     <- ``solve(A, b, c, x_b, b_ixs, m, n, t)`` (v4:219-380)
+* :class:`SolveStatus` <- ``enum class SolveStatus`` (v4:49-54)
+* :class:`Context`  step-wise / benchmark access to the same device loop
+  (``price`` = v4:288-302, ``pivot`` = v4:306-357).
+
+Everything computes through ``libsimplex.so`` (hand-written gfx950 HIP
+kernels behind the C-ABI in ``include/simplex.h``); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from enum import IntEnum
+
+import numpy as np
+
+from ._lib import SimplexError, SpxOpts, check, load
+
+__all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
+           "shard_range", "minloc_merge",
+           "SimplexError", "FLAG_TIMING"]
+
+FLAG_TIMING = 1
+
+
+class SolveStatus(IntEnum):
+    MaxIter = 0
+    OptimumFound = 1
+    Unbounded = 2
+    ThetaOverflow = 3
+
+
+@dataclass
+class SolveResult:
+    z: float
+    status: SolveStatus
+    x_b: np.ndarray
+    b_ixs: np.ndarray
+    pivots: int
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def read_lp(path: str):
+    """LP text format of the reference: ``m n``, A (m x n, row-major), b (m),
+    c (n); anything after c is ignored (input/sample.txt).  Returns
+    ``(m, n, A_cols, b, c)`` with ``A_cols`` shaped (n, m) — i.e. A stored
+    column-major, the layout the reference keeps on the device (R2C, v4:59-60)."""
+    with open(path) as f:
+        toks = f.read().split()
+    try:
+        m, n = int(toks[0]), int(toks[1])
+    except (IndexError, ValueError):
+        raise ValueError("Either failed to read m and n, or m > n.")
+    if m > n:
+        raise ValueError("Either failed to read m and n, or m > n.")
+    need = m * n + m + n
+    if len(toks) - 2 < need:
+        raise ValueError("truncated LP file")
+    vals = np.array(toks[2:2 + need], dtype=np.float64)
+    A_cols = np.ascontiguousarray(vals[: m * n].reshape(m, n).T)
+    return m, n, A_cols, vals[m * n: m * n + m].copy(), vals[m * n + m:].copy()
+
+
+def shard_range(m: int, n: int, rank: int, nranks: int):
+    """(s_lo, s_hi, k_lo, k_hi): this rank's structural and slack column blocks."""
+    out = (ctypes.c_int64 * 4)()
+    check(load().spx_shard_range(m, n, rank, nranks, out))
+    return tuple(out)
+
+
+def minloc_merge(vals, idx):
+    """Cross-rank MINLOC rule: smallest value, then smallest global index."""
+    v = np.ascontiguousarray(vals, dtype=np.float64)
+    i = np.ascontiguousarray(idx, dtype=np.int64)
+    bv, bi = ctypes.c_double(), ctypes.c_int64()
+    check(load().spx_minloc_merge(_ptr(v), _ptr(i), len(v), ctypes.byref(bv), ctypes.byref(bi)))
+    return bv.value, bi.value
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    check(load().spx_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Context:
+    """One device-resident LP (``spx_ctx``).  Either pass ``A_cols`` (n, m),
+    ``b``, ``c`` or ``m, n, seed`` for the seeded generator of SURVEY.md §8(d)."""
+
+    def __init__(self, A_cols=None, b=None, c=None, *, m: int | None = None, n: int | None = None,
+                 seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
+                 nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
+                 update_rows: int = 0, price_grid: int = 0):
+        L = load()
+        o = SpxOpts()
+        L.spx_default_opts(ctypes.byref(o))
+        o.eps, o.device, o.rank, o.nranks = eps, device, rank, nranks
+        o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
+        o.flags = FLAG_TIMING if timing else 0
+        h = ctypes.c_void_p()
+        if A_cols is not None:
+            A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
+            n_, m_ = A_cols.shape
+            b = np.ascontiguousarray(b, dtype=np.float64)
+            c = np.ascontiguousarray(c, dtype=np.float64)
+            if b.shape != (m_,) or c.shape != (n_,):
+                raise ValueError("shape mismatch: A_cols (n, m), b (m,), c (n,)")
+            check(L.spx_create(ctypes.byref(h), m_, n_, _ptr(A_cols), _ptr(b), _ptr(c), ctypes.byref(o)))
+            self.m, self.n = m_, n_
+        else:
+            if m is None or n is None or seed is None:
+                raise ValueError("give A_cols, b, c or m, n, seed")
+            check(L.spx_create_generated(ctypes.byref(h), m, n, seed, ctypes.byref(o)))
+            self.m, self.n = m, n
+        self._h = h
+        self._L = L
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.spx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def attach_comm(self, uid: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self._L.spx_attach_comm(self._h, buf))
+
+    def reset(self):
+        check(self._L.spx_reset(self._h))
+
+    # -- loop
+    def iterate(self, k: int):
+        st, piv = ctypes.c_int32(), ctypes.c_int64()
+        check(self._L.spx_iterate(self._h, k, ctypes.byref(st), ctypes.byref(piv)))
+        return SolveStatus(st.value), piv.value
+
+    def solve(self, max_iter: int = (1 << 62)) -> SolveResult:
+        z, st, piv = ctypes.c_double(), ctypes.c_int32(), ctypes.c_int64()
+        x_b = np.zeros(self.m)
+        b_ixs = np.zeros(self.m, dtype=np.int64)
+        check(self._L.spx_solve(self._h, max_iter, ctypes.byref(z), _ptr(b_ixs), _ptr(x_b),
+                                ctypes.byref(st), ctypes.byref(piv)))
+        return SolveResult(z.value, SolveStatus(st.value), x_b, b_ixs, piv.value)
+
+    def price(self):
+        p, e, opt = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int32()
+        check(self._L.spx_price(self._h, ctypes.byref(p), ctypes.byref(e), ctypes.byref(opt)))
+        return p.value, e.value, bool(opt.value)
+
+    def pivot(self):
+        q, st = ctypes.c_int64(), ctypes.c_int32()
+        check(self._L.spx_pivot(self._h, ctypes.byref(q), ctypes.byref(st)))
+        return q.value, SolveStatus(st.value)
+
+    # -- readback
+    def state(self, binv: bool = False):
+        m = self.m
+        out = {"x_b": np.zeros(m), "b_ixs": np.zeros(m, dtype=np.int64), "y": np.zeros(m),
+               "c_B": np.zeros(m), "binv": np.zeros((m, m)) if binv else None}
+        st, piv = ctypes.c_int32(), ctypes.c_int64()
+        check(self._L.spx_get_state(self._h, _ptr(out["x_b"]), _ptr(out["b_ixs"]), _ptr(out["y"]),
+                                    _ptr(out["c_B"]), _ptr(out["binv"]), ctypes.byref(st), ctypes.byref(piv)))
+        out["status"] = SolveStatus(st.value)
+        out["pivots"] = piv.value
+        return out
+
+    def reduced_costs(self) -> np.ndarray:
+        e = np.zeros(self.n)
+        check(self._L.spx_reduced_costs(self._h, _ptr(e)))
+        return e
+
+    def objective(self) -> float:
+        z = ctypes.c_double()
+        check(self._L.spx_objective(self._h, ctypes.byref(z)))
+        return z.value
+
+    def kernel_times(self):
+        tp, tu, np_, nu = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.spx_kernel_times(self._h, ctypes.byref(tp), ctypes.byref(np_), ctypes.byref(tu),
+                                       ctypes.byref(nu)))
+        return {"price_ms": tp.value, "price_launches": np_.value,
+                "update_ms": tu.value, "update_launches": nu.value}
+
+    def info(self):
+        m, n, ld, nb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        bp, bu = ctypes.c_double(), ctypes.c_double()
+        check(self._L.spx_info(self._h, ctypes.byref(m), ctypes.byref(n), ctypes.byref(ld), ctypes.byref(nb),
+                               ctypes.byref(bp), ctypes.byref(bu)))
+        return {"m": m.value, "n": n.value, "ld": ld.value, "local_nonbasic": nb.value,
+                "bytes_price": bp.value, "bytes_update": bu.value}
+
+
+def solve(A_cols, b, c, max_iter: int = (1 << 62), eps: float = 1e-7, device: int = -1) -> SolveResult:
+    """Mirror of the reference's ``solve()`` (v4:219-380): A column-major as
+    (n, m), returns z, status, x_b and b_ixs in basis order, pivots made."""
+    with Context(A_cols, b, c, eps=eps, device=device) as ctx:
+        return ctx.solve(max_iter)

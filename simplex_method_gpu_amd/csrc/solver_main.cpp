@@ -1,0 +1,201 @@
+// solver_main.cpp — `./solver <file>` CLI, the drop-in for the reference's
+// bin/solverN.out (main() at src/v4_cub_reduction.cu:384-473).
+//
+// Same argv, same LP text format (m n, A row-major, b, c; trailing text
+// ignored — reader at v4:94-104, 401-419), same stdout: "# Iteration k" per
+// loop pass (v4:136-142), the result block (v4:426-445) and the timing table
+// (v4:456-471).  Compute goes through libsimplex's C-ABI only.
+//
+// Extra flags (all optional, before the file):
+//   --max-iter K   loop passes (default: unlimited; reference MAX_ITER=5, v4:19)
+//   --eps E        optimality tolerance (default 1e-7; reference 1e-4 f32, v4:18)
+//   --compat       reference constants: --max-iter 5 --eps 1e-4
+//   --gen m n seed solve the seeded random LP of SURVEY.md §8(d) (no file)
+//   --device D     HIP device ordinal
+//   --no-iter-lines  suppress the "# Iteration k" lines
+//   --json         also print one JSON result line
+#include <chrono>
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/simplex.h"
+
+using Clock = std::chrono::steady_clock;
+using TimePoint = Clock::time_point;
+
+static double seconds(const TimePoint& a, const TimePoint& b) { return std::chrono::duration<double>(b - a).count(); }
+
+static void print_elapsed_time(const char* msg, double dur) {
+    auto label = std::string(msg) + ": ";
+    std::cout << std::setw(19) << label;
+    std::cout << std::fixed << std::setprecision(2);
+    std::cout << std::setw(6) << dur << '\n';
+}
+
+static bool load_matrix(std::ifstream& file, double* a, int64_t m, int64_t n, const char* name) {
+    // row-major text -> column-major storage (R2C, v4:59-60,94-104)
+    for (int64_t i = 0; i < m; ++i)
+        for (int64_t j = 0; j < n; ++j)
+            if (!(file >> a[i + j * m])) {
+                std::cerr << "Failed to read (" << i << "," << j << ") for " << name << "\n";
+                return false;
+            }
+    return true;
+}
+
+static void usage() {
+    std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
+                 " (<file> | --gen m n seed)\n";
+}
+
+int main(int argc, char* argv[]) {
+    std::ios_base::sync_with_stdio(false);
+    int64_t max_iter = INT64_MAX;
+    double eps = 1e-7;
+    int device = -1;
+    bool iter_lines = true, json = false, gen = false;
+    int64_t gm = 0, gn = 0;
+    uint64_t gseed = 0;
+    const char* path = nullptr;
+    for (int a = 1; a < argc; ++a) {
+        const std::string s = argv[a];
+        auto need = [&](int k) {
+            if (a + k >= argc) {
+                usage();
+                std::exit(1);
+            }
+        };
+        if (s == "--max-iter") { need(1); max_iter = std::strtoll(argv[++a], nullptr, 10); }
+        else if (s == "--eps") { need(1); eps = std::strtod(argv[++a], nullptr); }
+        else if (s == "--compat") { max_iter = 5; eps = 1e-4; }
+        else if (s == "--device") { need(1); device = std::atoi(argv[++a]); }
+        else if (s == "--no-iter-lines") iter_lines = false;
+        else if (s == "--json") json = true;
+        else if (s == "--gen") {
+            need(3);
+            gen = true;
+            gm = std::strtoll(argv[++a], nullptr, 10);
+            gn = std::strtoll(argv[++a], nullptr, 10);
+            gseed = std::strtoull(argv[++a], nullptr, 10);
+        } else if (s == "-h" || s == "--help") { usage(); return 0; }
+        else if (!path) path = argv[a];
+        else { usage(); return 1; }
+    }
+    if (!path && !gen) {
+        std::cerr << "Please, specify an input file.\n";
+        return 1;
+    }
+
+    const TimePoint t_start = Clock::now();
+    TimePoint t_host_alloc = t_start, t_read = t_start, t_solve = t_start;
+    int64_t m = 0, n = 0;
+    std::vector<double> A, b, c;
+    if (!gen) {
+        std::ifstream file(path);
+        if (!file.is_open()) {
+            std::cerr << "Could not open " << path << ".\n";
+            return 1;
+        }
+        if (!(file >> m >> n) || m > n) {
+            std::cerr << "Either failed to read m and n, or m > n.\n";
+            return 1;
+        }
+        t_host_alloc = Clock::now();
+        A.resize((size_t)(m * n));
+        b.resize((size_t)m);
+        c.resize((size_t)n);
+        t_read = Clock::now();
+        if (!load_matrix(file, A.data(), m, n, "A") || !load_matrix(file, b.data(), m, 1, "b") ||
+            !load_matrix(file, c.data(), 1, n, "c"))
+            return EXIT_FAILURE;
+    } else {
+        m = gm;
+        n = gn;
+        t_host_alloc = t_read = Clock::now();
+    }
+    std::vector<double> x_b((size_t)std::max<int64_t>(m, 1));
+    std::vector<int64_t> b_ixs((size_t)std::max<int64_t>(m, 1));
+
+    t_solve = Clock::now();
+    spx_opts o;
+    spx_default_opts(&o);
+    o.eps = eps;
+    o.device = device;
+    spx_ctx* ctx = nullptr;
+    const TimePoint t_alloc = Clock::now();
+    int rc = gen ? spx_create_generated(&ctx, m, n, gseed, &o)
+                 : spx_create(&ctx, m, n, A.data(), b.data(), c.data(), &o);
+    if (rc != SPX_OK) {
+        std::cerr << "spx_create failed (" << rc << "): " << spx_last_error() << "\n";
+        return EXIT_FAILURE;
+    }
+    const TimePoint t_init_end = Clock::now();
+    double z = 0.0;
+    int32_t status = 0;
+    int64_t pivots = 0;
+    rc = spx_solve(ctx, max_iter, &z, b_ixs.data(), x_b.data(), &status, &pivots);
+    if (rc != SPX_OK) {
+        std::cerr << "spx_solve failed (" << rc << "): " << spx_last_error() << "\n";
+        spx_destroy(ctx);
+        return EXIT_FAILURE;
+    }
+    const TimePoint t_loop_end = Clock::now();
+    spx_destroy(ctx);
+    const TimePoint t_dealloc_end = Clock::now();
+
+    // "# Iteration k" once per loop pass (v4:287): pivots + the terminating pass
+    const int64_t passes = (status == SPX_STATUS_MAX_ITER) ? pivots : pivots + 1;
+    if (iter_lines)
+        for (int64_t i = 1; i <= passes; ++i) std::cout << "# Iteration " << i << '\n';
+
+    const TimePoint t_print = Clock::now();
+    switch (status) {
+        case SPX_STATUS_OPTIMUM_FOUND:
+            std::cout << "Optimum found: " << z << '\n';
+            for (int64_t i = 0; i < m; ++i) std::cout << "\tx_" << b_ixs[(size_t)i] << " = " << x_b[(size_t)i] << "\n";
+            break;
+        case SPX_STATUS_UNBOUNDED: std::cout << "Problem unbounded.\n"; break;
+        case SPX_STATUS_THETA_OVERFLOW: std::cout << "Theta overflow.\n"; break;
+        default: std::cout << "MAX_ITER exceeded.\n"; break;
+    }
+    std::cout << '\n';
+    const TimePoint t_host_free = Clock::now();
+    A.clear();
+    A.shrink_to_fit();
+    const TimePoint t_end = Clock::now();
+
+    // timing table (v4:456-471).  The reference's y / x_b phases are fused into
+    // the update kernel here, so the whole device loop is reported under p and
+    // B_inv is 0 (per-kernel device times: bench.py / spx_kernel_times).
+    print_elapsed_time("Total", seconds(t_start, t_end));
+    std::cout << '\n';
+    print_elapsed_time("y", 0.0);
+    print_elapsed_time("p", seconds(t_init_end, t_loop_end));
+    print_elapsed_time("B_inv", 0.0);
+    print_elapsed_time("x_b", 0.0);
+    std::cout << '\n';
+    print_elapsed_time("Alloc", seconds(t_alloc, t_init_end));
+    print_elapsed_time("Init", 0.0);
+    print_elapsed_time("Dealloc", seconds(t_loop_end, t_dealloc_end));
+    std::cout << '\n';
+    print_elapsed_time("Host alloc", seconds(t_host_alloc, t_read));
+    print_elapsed_time("Read file", seconds(t_read, t_solve));
+    print_elapsed_time("Solve call", seconds(t_solve, t_print));
+    print_elapsed_time("Print result", seconds(t_print, t_host_free));
+    print_elapsed_time("Host free", seconds(t_host_free, t_end));
+
+    if (json) {
+        std::cout << std::defaultfloat << std::setprecision(17);
+        std::cout << "{\"status\": " << status << ", \"z\": " << z << ", \"pivots\": " << pivots
+                  << ", \"m\": " << m << ", \"n\": " << n
+                  << ", \"solve_s\": " << seconds(t_init_end, t_loop_end) << "}\n";
+    }
+    return 0;
+}

@@ -1,0 +1,603 @@
+// spx_api.cpp — host runtime behind include/simplex.h.
+//
+// Replaces the reference's solve() (src/v4_cub_reduction.cu:219-380): device
+// allocation, upload, slack-basis init, the iteration loop and readback.  The
+// loop differs in shape, not in meaning: the reference blocks on 4 D2H reads
+// per pass (v4:295,296,317,325) and issues ~20 cuBLAS/CUB/kernel calls; here a
+// pass is two kernels, termination is a device-side status word, and batches
+// of passes are replayed from one captured hipGraph with a single
+// synchronisation per batch.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/simplex.h"
+#include "spx_device.h"
+#include "spx_kernels.h"
+
+using namespace spx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(e_ == hipErrorOutOfMemory ? SPX_ERR_OOM : SPX_ERR_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                    \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                                  \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess)                                                                          \
+            return fail(SPX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__); \
+    } while (0)
+
+#define SPX_TRY(expr)          \
+    do {                       \
+        int rc_ = (expr);      \
+        if (rc_ != SPX_OK) return rc_; \
+    } while (0)
+
+int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Structural columns [0, ns) and slack columns [ns, n) are each cut into
+// nranks contiguous blocks, so the initial slack basis is spread evenly.
+void shard_range(int64_t m, int64_t n, int r, int G, int64_t out[4]) {
+    const int64_t ns = n - m;
+    const int64_t sb = (ns + G - 1) / G, kb = (m + G - 1) / G;
+    out[0] = std::min<int64_t>(ns, (int64_t)r * sb);
+    out[1] = std::min<int64_t>(ns, (int64_t)(r + 1) * sb);
+    out[2] = ns + std::min<int64_t>(m, (int64_t)r * kb);
+    out[3] = ns + std::min<int64_t>(m, (int64_t)(r + 1) * kb);
+}
+
+}  // namespace
+
+struct spx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int cus = 256;
+    int64_t m = 0, n = 0, L = 0, ns = 0;
+    spx_opts opts{};
+    Params P{};
+    PriceCfg pcfg{};
+    UpdateCfg ucfg{};
+    int64_t max_local_cols = 0;
+
+    // device allocations
+    std::vector<void*> allocs;
+    double* A = nullptr;
+    double* b = nullptr;
+    double* c = nullptr;
+    ArgMinEntry* send = nullptr;
+    ArgMinEntry* recv = nullptr;
+
+    // pinned host mirrors
+    DevState* st_host = nullptr;
+    int64_t* limit_host = nullptr;
+
+    // multi-rank
+    ncclComm_t comm = nullptr;
+    bool comm_ready = false;
+
+    // graph replay of `batch` passes
+    hipGraphExec_t graph_exec = nullptr;
+    hipGraph_t graph = nullptr;
+    int batch = 0;
+
+    // per-kernel timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_price, ev_update;  // pairs (start, stop)
+    size_t n_price = 0, n_update = 0;
+
+    int64_t pivots = 0;
+    int32_t status = SPX_STATUS_MAX_ITER;
+    bool stepped_price = false;
+
+    template <typename T>
+    int alloc(T** p, size_t count) {
+        void* d = nullptr;
+        size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e != hipSuccess) return fail(SPX_ERR_OOM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+        allocs.push_back(d);
+        e = hipMemsetAsync(d, 0, bytes, stream);
+        if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(e));
+        *p = static_cast<T*>(d);
+        return SPX_OK;
+    }
+};
+
+extern "C" {
+
+void spx_default_opts(spx_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->eps = 1e-7;
+    o->device = -1;
+    o->rank = 0;
+    o->nranks = 1;
+    o->graph_batch = 0;
+}
+
+const char* spx_last_error(void) { return g_err.c_str(); }
+
+int spx_abi_version(void) { return SPX_ABI_VERSION; }
+
+const char* spx_status_string(int32_t s) {
+    switch (s) {
+        case SPX_STATUS_MAX_ITER: return "MAX_ITER exceeded.";
+        case SPX_STATUS_OPTIMUM_FOUND: return "Optimum found";
+        case SPX_STATUS_UNBOUNDED: return "Problem unbounded.";
+        case SPX_STATUS_THETA_OVERFLOW: return "Theta overflow.";
+    }
+    return "unknown";
+}
+
+}  // extern "C"
+
+namespace {
+
+int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
+    if (opts) x->opts = *opts; else spx_default_opts(&x->opts);
+    if (x->opts.nranks < 1 || x->opts.rank < 0 || x->opts.rank >= x->opts.nranks)
+        return fail(SPX_ERR_ARG, "bad rank %d / nranks %d", x->opts.rank, x->opts.nranks);
+    if (!(x->opts.eps >= 0.0)) return fail(SPX_ERR_ARG, "eps must be >= 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SPX_ERR_NO_DEVICE, "no HIP device visible");
+    if (x->opts.device >= 0) {
+        if (x->opts.device >= ndev) return fail(SPX_ERR_ARG, "device %d out of range (%d)", x->opts.device, ndev);
+        HIP_TRY(hipSetDevice(x->opts.device));
+    }
+    HIP_TRY(hipGetDevice(&x->device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, x->device));
+    x->cus = prop.multiProcessorCount;
+    HIP_TRY(hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&x->st_host), sizeof(DevState), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&x->limit_host), sizeof(int64_t), hipHostMallocDefault));
+    std::memset(x->st_host, 0, sizeof(DevState));
+
+    x->m = m;
+    x->n = n;
+    x->ns = n - m;
+    x->L = round_up(m, 128);
+    x->timing = (x->opts.flags & SPX_FLAG_TIMING) != 0;
+    const int64_t L = x->L;
+    const int G = x->opts.nranks, r = x->opts.rank;
+
+    SPX_TRY(x->alloc(&x->A, (size_t)(L * n)));
+    SPX_TRY(x->alloc(&x->b, (size_t)L));
+    SPX_TRY(x->alloc(&x->c, (size_t)n));
+
+    Params& P = x->P;
+    P.A = x->A;
+    P.b = x->b;
+    P.c = x->c;
+    P.m = m;
+    P.n = n;
+    P.L = L;
+    P.ns = x->ns;
+    P.eps = x->opts.eps;
+    SPX_TRY(x->alloc(&P.B0, (size_t)(m * L)));
+    SPX_TRY(x->alloc(&P.B1, (size_t)(m * L)));
+    SPX_TRY(x->alloc(&P.E0, (size_t)L));
+    SPX_TRY(x->alloc(&P.E1, (size_t)L));
+    SPX_TRY(x->alloc(&P.r0, (size_t)L));
+    SPX_TRY(x->alloc(&P.r1, (size_t)L));
+    SPX_TRY(x->alloc(&P.y, (size_t)L));
+    SPX_TRY(x->alloc(&P.x_b, (size_t)L));
+    SPX_TRY(x->alloc(&P.c_B, (size_t)L));
+    SPX_TRY(x->alloc(&P.alpha, (size_t)L));
+    SPX_TRY(x->alloc(&P.b_ixs, (size_t)m));
+    SPX_TRY(x->alloc(&P.nb_list, (size_t)n));
+    SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
+    SPX_TRY(x->alloc(&P.st, 1));
+
+    // column shard: structural and slack columns each split in G contiguous blocks
+    int64_t rng[4];
+    shard_range(m, n, r, G, rng);
+    P.s_lo = rng[0];
+    P.s_hi = rng[1];
+    P.k_lo = rng[2];
+    P.k_hi = rng[3];
+    x->max_local_cols = (P.s_hi - P.s_lo) + (P.k_hi - P.k_lo);
+
+    // pricing geometry: y in LDS when it fits, 16 waves per CU either way
+    PriceCfg& pc = x->pcfg;
+    const size_t ybytes = (size_t)L * 8;
+    if (x->opts.price_block == 256 || x->opts.price_block == 512 || x->opts.price_block == 1024)
+        pc.block = x->opts.price_block;
+    else
+        pc.block = ybytes <= 40 * 1024 ? 256 : (ybytes <= 72 * 1024 ? 512 : 1024);
+    pc.lds_y = ybytes + (size_t)pc.block * 16 + 16 <= 150 * 1024;
+    pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (size_t)pc.block * sizeof(ArgMinEntry) + 16;
+    int per_cu = 0;
+    HIP_TRY(price_prepare(pc, &per_cu));
+    if (per_cu < 1) per_cu = 1;
+    const int waves = pc.block / 64;
+    int64_t want = (x->max_local_cols + waves - 1) / waves;
+    int64_t cap = (int64_t)x->cus * per_cu;
+    pc.grid = (int)std::max<int64_t>(1, std::min(want, cap));
+    if (x->opts.price_grid > 0) pc.grid = x->opts.price_grid;
+
+    UpdateCfg& uc = x->ucfg;
+    int rows = x->opts.update_rows;
+    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = (m >= 8192) ? 4 : (m >= 2048 ? 2 : 1);
+    uc.rows = rows;
+    uc.grid = (int)std::max<int64_t>(1, (m + 4 * rows - 1) / (4 * rows));
+
+    SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
+    SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
+    SPX_TRY(x->alloc(&x->send, 1));
+    SPX_TRY(x->alloc(&x->recv, (size_t)G));
+    P.price_out = x->send;
+    P.price_in = (G == 1) ? x->send : x->recv;
+    P.nin = G;
+
+    int gb = x->opts.graph_batch;
+    if (gb == 0) gb = 16;
+    x->batch = (gb < 0 || x->timing) ? 0 : gb;
+    return SPX_OK;
+}
+
+int do_reset(spx_ctx* x) {
+    const size_t mb = (size_t)(x->m * x->L) * sizeof(double);
+    HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
+    HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
+    for (double* v : {x->P.E0, x->P.E1, x->P.r0, x->P.r1, x->P.y, x->P.x_b, x->P.c_B, x->P.alpha})
+        HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
+    HIP_TRY(launch_reset(x->P, x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    x->pivots = 0;
+    x->status = SPX_STATUS_MAX_ITER;
+    x->stepped_price = false;
+    return SPX_OK;
+}
+
+// One loop pass: pricing, (MINLOC exchange), fused update.
+int enqueue_pass(spx_ctx* x, bool timed) {
+    hipEvent_t p0 = nullptr, p1 = nullptr, u0 = nullptr, u1 = nullptr;
+    if (timed) {
+        if (x->ev_price.size() < 2 * (x->n_price + 1)) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t e;
+                HIP_TRY(hipEventCreate(&e));
+                x->ev_price.push_back(e);
+            }
+        }
+        if (x->ev_update.size() < 2 * (x->n_update + 1)) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t e;
+                HIP_TRY(hipEventCreate(&e));
+                x->ev_update.push_back(e);
+            }
+        }
+        p0 = x->ev_price[2 * x->n_price];
+        p1 = x->ev_price[2 * x->n_price + 1];
+        u0 = x->ev_update[2 * x->n_update];
+        u1 = x->ev_update[2 * x->n_update + 1];
+        ++x->n_price;
+        ++x->n_update;
+    }
+    HIP_TRY(launch_price(x->P, x->pcfg, x->stream, p0, p1));
+    if (x->opts.nranks > 1) {
+        if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
+        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry), ncclUint8, x->comm, x->stream));
+    }
+    HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
+    return SPX_OK;
+}
+
+int build_graph(spx_ctx* x) {
+    if (x->graph_exec || x->batch <= 0) return SPX_OK;
+    HIP_TRY(hipStreamBeginCapture(x->stream, hipStreamCaptureModeThreadLocal));
+    int rc = SPX_OK;
+    for (int i = 0; i < x->batch && rc == SPX_OK; ++i) rc = enqueue_pass(x, false);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(x->stream, &g);
+    if (rc != SPX_OK) return rc;
+    if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    x->graph = g;
+    HIP_TRY(hipGraphInstantiate(&x->graph_exec, g, nullptr, nullptr, 0));
+    return SPX_OK;
+}
+
+int read_state(spx_ctx* x) {
+    HIP_TRY(hipMemcpyAsync(x->st_host, x->P.st, sizeof(DevState), hipMemcpyDeviceToHost, x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    x->pivots = x->st_host->iter;
+    x->status = x->st_host->status;  // ST_RUNNING == SPX_STATUS_MAX_ITER
+    return SPX_OK;
+}
+
+int set_limit(spx_ctx* x, int64_t limit) {
+    *x->limit_host = limit;
+    HIP_TRY(hipMemcpyAsync(&x->P.st->limit, x->limit_host, sizeof(int64_t), hipMemcpyHostToDevice, x->stream));
+    return SPX_OK;
+}
+
+int iterate(spx_ctx* x, int64_t k) {
+    if (x->status != SPX_STATUS_MAX_ITER || k <= 0) return SPX_OK;
+    if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
+    SPX_TRY(set_limit(x, x->pivots + k));
+    if (x->batch > 0) {
+        SPX_TRY(build_graph(x));
+        const int64_t reps = (k + x->batch - 1) / x->batch;
+        for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
+    } else {
+        for (int64_t i = 0; i < k; ++i) SPX_TRY(enqueue_pass(x, x->timing));
+    }
+    return read_state(x);
+}
+
+int create_tail(spx_ctx* x) {
+    SPX_TRY(do_reset(x));
+    return SPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const double* b, const double* c,
+               const spx_opts* opts) {
+    if (!out) return fail(SPX_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (m <= 0 || n < m) return fail(SPX_ERR_ARG, "Either failed to read m and n, or m > n. (m=%lld n=%lld)",
+                                     (long long)m, (long long)n);
+    if (n > (int64_t)0x7fffffff) return fail(SPX_ERR_ARG, "n too large");
+    if (!A || !b || !c) return fail(SPX_ERR_ARG, "NULL input array");
+    spx_ctx* x = new spx_ctx();
+    int rc = setup_common(x, m, n, opts);
+    if (rc == SPX_OK) {
+        hipError_t e = hipMemcpy2DAsync(x->A, (size_t)x->L * 8, A, (size_t)m * 8, (size_t)m * 8, (size_t)n,
+                                        hipMemcpyHostToDevice, x->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(x->b, b, (size_t)m * 8, hipMemcpyHostToDevice, x->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice, x->stream);
+        if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
+    }
+    if (rc == SPX_OK) rc = create_tail(x);
+    if (rc != SPX_OK) {
+        std::string keep = g_err;
+        spx_destroy(x);
+        g_err = keep;
+        return rc;
+    }
+    *out = x;
+    return SPX_OK;
+}
+
+int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed, const spx_opts* opts) {
+    if (!out) return fail(SPX_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (m <= 0 || n < m) return fail(SPX_ERR_ARG, "m must be in [1, n] (m=%lld n=%lld)", (long long)m, (long long)n);
+    if (n > (int64_t)0x7fffffff) return fail(SPX_ERR_ARG, "n too large");
+    spx_ctx* x = new spx_ctx();
+    int rc = setup_common(x, m, n, opts);
+    if (rc == SPX_OK) {
+        hipError_t e = launch_generate(x->A, x->b, x->c, m, n, x->L, seed, x->stream);
+        if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "generate failed: %s", hipGetErrorString(e));
+    }
+    if (rc == SPX_OK) rc = create_tail(x);
+    if (rc != SPX_OK) {
+        std::string keep = g_err;
+        spx_destroy(x);
+        g_err = keep;
+        return rc;
+    }
+    *out = x;
+    return SPX_OK;
+}
+
+void spx_destroy(spx_ctx* x) {
+    if (!x) return;
+    if (x->stream) (void)hipStreamSynchronize(x->stream);
+    if (x->graph_exec) (void)hipGraphExecDestroy(x->graph_exec);
+    if (x->graph) (void)hipGraphDestroy(x->graph);
+    for (hipEvent_t e : x->ev_price) (void)hipEventDestroy(e);
+    for (hipEvent_t e : x->ev_update) (void)hipEventDestroy(e);
+    if (x->comm) (void)ncclCommDestroy(x->comm);
+    for (void* p : x->allocs) (void)hipFree(p);
+    if (x->st_host) (void)hipHostFree(x->st_host);
+    if (x->limit_host) (void)hipHostFree(x->limit_host);
+    if (x->stream) (void)hipStreamDestroy(x->stream);
+    delete x;
+}
+
+int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]) {
+    if (!id) return fail(SPX_ERR_ARG, "id is NULL");
+    static_assert(sizeof(ncclUniqueId) <= SPX_COMM_ID_BYTES, "ncclUniqueId too large");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    std::memset(id, 0, SPX_COMM_ID_BYTES);
+    std::memcpy(id, &u, sizeof(u));
+    return SPX_OK;
+}
+
+int spx_attach_comm(spx_ctx* x, const uint8_t id[SPX_COMM_ID_BYTES]) {
+    if (!x || !id) return fail(SPX_ERR_ARG, "NULL argument");
+    if (x->opts.nranks == 1) return SPX_OK;
+    if (x->comm_ready) return fail(SPX_ERR_STATE, "communicator already attached");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    HIP_TRY(hipSetDevice(x->device));
+    NCCL_TRY(ncclCommInitRank(&x->comm, x->opts.nranks, u, x->opts.rank));
+    x->comm_ready = true;
+    return SPX_OK;
+}
+
+int spx_reset(spx_ctx* x) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    return do_reset(x);
+}
+
+int spx_iterate(spx_ctx* x, int64_t k, int32_t* status, int64_t* pivots) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    SPX_TRY(iterate(x, k));
+    if (status) *status = x->status;
+    if (pivots) *pivots = x->pivots;
+    return SPX_OK;
+}
+
+int spx_objective(spx_ctx* x, double* z) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    HIP_TRY(launch_objective(x->P, x->stream));
+    SPX_TRY(read_state(x));
+    if (z) *z = x->st_host->z;
+    return SPX_OK;
+}
+
+int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_b, double* binv, int32_t* status,
+                  int64_t* pivots) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    const size_t mb = (size_t)x->m * 8;
+    if (x_b) HIP_TRY(hipMemcpyAsync(x_b, x->P.x_b, mb, hipMemcpyDeviceToHost, x->stream));
+    if (b_ixs) HIP_TRY(hipMemcpyAsync(b_ixs, x->P.b_ixs, mb, hipMemcpyDeviceToHost, x->stream));
+    if (y) HIP_TRY(hipMemcpyAsync(y, x->P.y, mb, hipMemcpyDeviceToHost, x->stream));
+    if (c_b) HIP_TRY(hipMemcpyAsync(c_b, x->P.c_B, mb, hipMemcpyDeviceToHost, x->stream));
+    if (binv) {
+        double* tmp = nullptr;
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)(x->m * x->L) * 8, x->stream));
+        HIP_TRY(launch_materialize(x->P, tmp, x->stream));
+        HIP_TRY(hipMemcpy2DAsync(binv, mb, tmp, (size_t)x->L * 8, mb, (size_t)x->m, hipMemcpyDeviceToHost, x->stream));
+        HIP_TRY(hipFreeAsync(tmp, x->stream));
+    }
+    SPX_TRY(read_state(x));
+    if (status) *status = x->status;
+    if (pivots) *pivots = x->pivots;
+    return SPX_OK;
+}
+
+int spx_reduced_costs(spx_ctx* x, double* e) {
+    if (!x || !e) return fail(SPX_ERR_ARG, "NULL argument");
+    double* tmp = nullptr;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)x->n * 8, x->stream));
+    HIP_TRY(launch_reduced_costs(x->P, tmp, x->stream));
+    HIP_TRY(hipMemcpyAsync(e, tmp, (size_t)x->n * 8, hipMemcpyDeviceToHost, x->stream));
+    HIP_TRY(hipFreeAsync(tmp, x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    return SPX_OK;
+}
+
+int spx_solve(spx_ctx* x, int64_t max_iter, double* z, int64_t* b_ixs, double* x_b, int32_t* status,
+              int64_t* pivots) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (max_iter < 0) return fail(SPX_ERR_ARG, "max_iter < 0");
+    int64_t chunk = 16;
+    while (x->status == SPX_STATUS_MAX_ITER && x->pivots < max_iter) {
+        const int64_t k = std::min(chunk, max_iter - x->pivots);
+        SPX_TRY(iterate(x, k));
+        chunk = std::min<int64_t>(chunk * 2, 2048);
+    }
+    if (z) SPX_TRY(spx_objective(x, z));
+    SPX_TRY(spx_get_state(x, x_b, b_ixs, nullptr, nullptr, nullptr, status, pivots));
+    return SPX_OK;
+}
+
+int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (x->status != SPX_STATUS_MAX_ITER) return fail(SPX_ERR_STATE, "solve already terminated");
+    SPX_TRY(set_limit(x, x->pivots + 1));
+    HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
+    if (x->opts.nranks > 1) {
+        if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
+        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry), ncclUint8, x->comm, x->stream));
+    }
+    std::vector<ArgMinEntry> cand((size_t)x->opts.nranks);
+    HIP_TRY(hipMemcpyAsync(cand.data(), x->P.price_in, sizeof(ArgMinEntry) * cand.size(), hipMemcpyDeviceToHost,
+                           x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    ArgMinEntry best{INFINITY, INT64_MAX};
+    for (const ArgMinEntry& e : cand)
+        if (argmin_better(e.val, e.idx, best.val, best.idx)) best = e;
+    if (p) *p = (best.idx == INT64_MAX) ? -1 : best.idx;
+    if (min_e) *min_e = best.val;
+    if (optimal) *optimal = (best.val >= -x->opts.eps || best.idx == INT64_MAX) ? 1 : 0;
+    x->stepped_price = true;
+    return SPX_OK;
+}
+
+int spx_pivot(spx_ctx* x, int64_t* q, int32_t* status) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (!x->stepped_price) return fail(SPX_ERR_STATE, "spx_pivot needs a preceding spx_price");
+    x->stepped_price = false;
+    HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
+    SPX_TRY(read_state(x));
+    if (q) *q = x->st_host->q;
+    if (status) *status = x->status;
+    return SPX_OK;
+}
+
+int spx_kernel_times(spx_ctx* x, double* price_ms, int64_t* np, double* update_ms, int64_t* nu) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    double tp = 0.0, tu = 0.0;
+    for (size_t i = 0; i < x->n_price; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, x->ev_price[2 * i], x->ev_price[2 * i + 1]));
+        tp += ms;
+    }
+    for (size_t i = 0; i < x->n_update; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, x->ev_update[2 * i], x->ev_update[2 * i + 1]));
+        tu += ms;
+    }
+    if (price_ms) *price_ms = tp;
+    if (update_ms) *update_ms = tu;
+    if (np) *np = (int64_t)x->n_price;
+    if (nu) *nu = (int64_t)x->n_update;
+    x->n_price = x->n_update = 0;
+    return SPX_OK;
+}
+
+int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb, double* bp, double* bu) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    SPX_TRY(read_state(x));
+    if (m) *m = x->m;
+    if (n) *n = x->n;
+    if (ld) *ld = x->L;
+    if (local_nb) *local_nb = x->st_host->nb_count;
+    if (bp) *bp = 8.0 * (double)(x->m + 1) * (double)x->st_host->nb_count;
+    if (bu) *bu = 16.0 * (double)x->m * (double)x->m;
+    return SPX_OK;
+}
+
+int spx_shard_range(int64_t m, int64_t n, int32_t rank, int32_t nranks, int64_t out[4]) {
+    if (!out || m <= 0 || n < m || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(SPX_ERR_ARG, "bad shard arguments");
+    shard_range(m, n, rank, nranks, out);
+    return SPX_OK;
+}
+
+int spx_minloc_merge(const double* vals, const int64_t* idx, int32_t count, double* best_val, int64_t* best_idx) {
+    if ((count > 0 && (!vals || !idx)) || !best_val || !best_idx) return fail(SPX_ERR_ARG, "NULL argument");
+    ArgMinEntry b{INFINITY, INT64_MAX};
+    for (int32_t g = 0; g < count; ++g)
+        if (argmin_better(vals[g], idx[g], b.val, b.idx)) b = ArgMinEntry{vals[g], idx[g]};
+    *best_val = b.val;
+    *best_idx = b.idx;
+    return SPX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+// spx_kernels.h — host-side launchers for the gfx950 kernels (spx_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "spx_device.h"
+
+namespace spx {
+
+struct PriceCfg {
+    int block;         // 256 / 512 / 1024 threads
+    bool lds_y;        // stage y in LDS (L*8 bytes) or read it from global
+    size_t lds_bytes;  // dynamic LDS per workgroup
+    int grid;          // workgroups (persistent-style, grid-stride over columns)
+};
+
+struct UpdateCfg {
+    int rows;  // B^-1 rows per wave (1/2/4/8); block is 256 threads
+    int grid;  // ceil(m / (4 * rows))
+};
+
+hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu);
+hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n, int64_t L, uint64_t seed,
+                           hipStream_t s);
+hipError_t launch_reset(const Params& P, hipStream_t s);
+hipError_t launch_materialize(const Params& P, double* out, hipStream_t s);
+hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s);
+hipError_t launch_objective(const Params& P, hipStream_t s);
+
+}  // namespace spx

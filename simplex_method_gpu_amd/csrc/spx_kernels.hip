@@ -1,0 +1,636 @@
+// spx_kernels.hip — gfx950 kernels of the dense revised-simplex hot loop.
+//
+// One loop pass is two launches (SURVEY.md §7 design notes):
+//   k_price   e_j = y.A_j - c_j over this rank's non-basic columns, fused with
+//             the entering argmin (v4:288-302).  One wave per column, A read
+//             with 16-byte loads, y staged once per workgroup in LDS, wave
+//             shuffle + LDS argmin, last-workgroup-done fan-in.
+//   k_update  applies the pending rank-1 update B^-1 += E r^T (v4:331-333)
+//             while streaming B^-1 once, and in the same pass computes
+//             FTRAN alpha = B^-1_new A_p (v4:307-308); fused compute_theta +
+//             leaving argmin (v4:199-208,324); the last workgroup then forms
+//             E_q (v4:210-215), the pivot row r, and updates x_b, y, c_B and
+//             the basis (v4:339-357).
+// Host synchronisation per pass: none.  Termination (optimum / unbounded /
+// iteration limit) is a device-side status word every kernel checks first.
+//
+// Cross-workgroup hand-offs inside a launch (partials, alpha) use agent-scope
+// relaxed atomic stores/loads (global_* sc1: L1 bypass) drained with
+// s_waitcnt vmcnt(0) before a workgroup barrier and one agent-scope ticket
+// add per workgroup (MI355X_MICROARCH.md, Valid forms, first table row).
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+#include <math.h>
+
+#include "spx_device.h"
+#include "spx_kernels.h"
+
+namespace spx {
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ bool stopped(const DevState* st) {
+    return st->status != ST_RUNNING || st->iter >= st->limit;
+}
+
+// ---------------------------------------------------------------------------
+// Pricing + entering argmin
+// ---------------------------------------------------------------------------
+template <int BLOCK, bool LDS_Y>
+__global__ __launch_bounds__(BLOCK) void k_price(Params P) {
+    DevState* st = P.st;
+    if (stopped(st)) return;
+    constexpr int WAVES = BLOCK / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int64_t L = P.L;
+    const int64_t L2 = L >> 1;
+    double* ys = reinterpret_cast<double*>(smem);
+    ArgMinEntry* red = reinterpret_cast<ArgMinEntry*>(smem + (LDS_Y ? L * 8 : 0));
+    int* s_last = reinterpret_cast<int*>(red + BLOCK);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    if constexpr (LDS_Y) {
+        const dbl2* yg = reinterpret_cast<const dbl2*>(P.y);
+        dbl2* yl = reinterpret_cast<dbl2*>(ys);
+        for (int64_t k = tid; k < L2; k += BLOCK) yl[k] = yg[k];
+        __syncthreads();
+    }
+    const dbl2* y2 = LDS_Y ? reinterpret_cast<const dbl2*>(ys) : reinterpret_cast<const dbl2*>(P.y);
+
+    const int nb = st->nb_count;
+    double best = INFINITY;
+    int64_t bj = INT64_MAX;
+    for (int idx = blockIdx.x * WAVES + wave; idx < nb; idx += gridDim.x * WAVES) {
+        const int64_t j = P.nb_list[idx];
+        const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
+        double a0 = 0.0, a1 = 0.0;
+        int64_t k = lane;
+        for (; k + 7 * 64 < L2; k += 8 * 64) {
+            dbl2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(&col[k + u * 64]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const dbl2 w = y2[k + u * 64];
+                a0 = fma(v[u].x, w.x, a0);
+                a1 = fma(v[u].y, w.y, a1);
+            }
+        }
+        for (; k < L2; k += 64) {
+            const dbl2 v = __builtin_nontemporal_load(&col[k]);
+            const dbl2 w = y2[k];
+            a0 = fma(v.x, w.x, a0);
+            a1 = fma(v.y, w.y, a1);
+        }
+        const double e = wave_sum(a0 + a1) - P.c[j];
+        if (argmin_better(e, j, best, bj)) { best = e; bj = j; }
+    }
+
+    // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
+    if (lane == 0) red[wave] = ArgMinEntry{best, bj};
+    __syncthreads();
+    if (tid == 0) {
+        ArgMinEntry w = red[0];
+        for (int i = 1; i < WAVES; ++i)
+            if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
+        st_agent(&P.price_partials[blockIdx.x].val, w.val);
+        st_agent(&P.price_partials[blockIdx.x].idx, w.idx);
+        drain_vmem();
+        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_price, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = (t == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!*s_last) return;
+
+    // last workgroup: reduce all partials
+    ArgMinEntry w{INFINITY, INT64_MAX};
+    for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
+        const double v = ld_agent(&P.price_partials[g].val);
+        const int64_t i = ld_agent(&P.price_partials[g].idx);
+        if (argmin_better(v, i, w.val, w.idx)) w = ArgMinEntry{v, i};
+    }
+    red[tid] = w;
+    __syncthreads();
+    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+        if (tid < s && argmin_better(red[tid + s].val, red[tid + s].idx, red[tid].val, red[tid].idx))
+            red[tid] = red[tid + s];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *P.price_out = red[0];
+        st_agent(&st->ticket_price, 0u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused: pending rank-1 update + FTRAN + ratio test + leaving argmin + tail
+// ---------------------------------------------------------------------------
+template <int BLOCK>
+__device__ void block_sum2(double& a, double& b, double* sa, double* sb) {
+    const int tid = threadIdx.x;
+    sa[tid] = a;
+    sb[tid] = b;
+    __syncthreads();
+    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            sa[tid] += sa[tid + s];
+            sb[tid] += sb[tid + s];
+        }
+        __syncthreads();
+    }
+    a = sa[0];
+    b = sb[0];
+    __syncthreads();
+}
+
+// Runs in the last workgroup of k_update: everything after the leaving argmin
+// (v4:317-357) on O(m) vectors.
+template <int BLOCK>
+__device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
+                            int par, unsigned char* smem) {
+    const int tid = threadIdx.x;
+    const int64_t m = P.m, L = P.L;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
+
+    // (1) leaving argmin over workgroup partials + unbounded count (v4:317-325)
+    UpdPartial w{INFINITY, INT64_MAX, 0, 0};
+    for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
+        const double th = ld_agent(&P.upd_partials[g].theta);
+        const int64_t i = ld_agent(&P.upd_partials[g].idx);
+        const int64_t np = ld_agent(&P.upd_partials[g].nonpos);
+        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
+        w.nonpos += np;
+    }
+    red[tid] = w;
+    __syncthreads();
+    for (int s = BLOCK / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            UpdPartial a = red[tid];
+            const UpdPartial bq = red[tid + s];
+            if (argmin_better(bq.theta, bq.idx, a.theta, a.idx)) { a.theta = bq.theta; a.idx = bq.idx; }
+            a.nonpos += bq.nonpos;
+            red[tid] = a;
+        }
+        __syncthreads();
+    }
+    const int64_t q = red[0].idx;
+    const int64_t nonpos = red[0].nonpos;
+    __syncthreads();
+    // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no valid
+    // candidate at all (NaN-poisoned x_b) stops the same way instead of
+    // indexing out of range.
+    if (nonpos == m || q < 0 || q >= m) {
+        if (tid == 0) {
+            st->p = p;
+            st->min_e = min_e;
+            st->q = -1;
+            st->status = ST_UNBOUNDED;
+            st_agent(&st->ticket_update, 0u);
+        }
+        return;
+    }
+
+    const double* Bsrc = par ? P.B1 : P.B0;
+    const double* Ep = par ? P.E1 : P.E0;
+    const double* rp = par ? P.r1 : P.r0;
+    double* Ec = par ? P.E0 : P.E1;
+    double* rc = par ? P.r0 : P.r1;
+
+    // (2) E_q (compute_E_q, v4:210-215)
+    const double aq = ld_agent(&P.alpha[q]);
+    for (int64_t i = tid; i < m; i += BLOCK) {
+        const double a = ld_agent(&P.alpha[i]);
+        Ec[i] = (i != q) ? (-a / aq) : (1.0 / aq - 1.0);
+    }
+    // (3) pivot row r = B^-1_new[q,:] (v4:331), recomputed exactly as the
+    //     streaming pass wrote it: fma(E_prev[q], r_prev[k], B_old[q,k])
+    const double eq = Ep[q];
+    const double* brow = Bsrc + q * L;
+    for (int64_t k = tid; k < L; k += BLOCK) rc[k] = fma(eq, rp[k], brow[k]);
+
+    // (4) s_x = r.b (v4:347), s_y = c_B_new.E_q (v4:354), c_B_new[q] = c_p
+    const double c_p = P.c[p];
+    double sx = 0.0, sy = 0.0;
+    for (int64_t k = tid; k < m; k += BLOCK) sx = fma(rc[k], P.b[k], sx);
+    for (int64_t i = tid; i < m; i += BLOCK) sy = fma((i == q) ? c_p : P.c_B[i], Ec[i], sy);
+    double* sa = reinterpret_cast<double*>(smem);
+    double* sb = sa + BLOCK;
+    block_sum2<BLOCK>(sx, sy, sa, sb);
+    const double c_bq = P.c_B[q];
+    const double s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+
+    // (5) x_b += s_x E_q (v4:348); y += s_y r (v4:356)
+    for (int64_t i = tid; i < m; i += BLOCK) P.x_b[i] = fma(sx, Ec[i], P.x_b[i]);
+    for (int64_t k = tid; k < m; k += BLOCK) P.y[k] = fma(s_y, rc[k], P.y[k]);
+    __syncthreads();
+
+    // (6) basis bookkeeping (v4:339-342) + non-basic list
+    if (tid == 0) {
+        const int64_t leave = P.b_ixs[q];
+        P.c_B[q] = c_p;
+        P.b_ixs[q] = p;
+        int cnt = st->nb_count;
+        if (owns_col(P, p)) {
+            const int kp = P.nb_pos[p];
+            const int last = P.nb_list[cnt - 1];
+            P.nb_list[kp] = last;
+            P.nb_pos[last] = kp;
+            P.nb_pos[p] = -1;
+            --cnt;
+        }
+        if (owns_col(P, leave)) {
+            P.nb_list[cnt] = (int32_t)leave;
+            P.nb_pos[leave] = cnt;
+            ++cnt;
+        }
+        st->nb_count = cnt;
+        st->p = p;
+        st->q = q;
+        st->min_e = min_e;
+        st->iter = it + 1;
+        st_agent(&st->ticket_update, 0u);
+    }
+}
+
+template <int BLOCK, int R>
+__global__ __launch_bounds__(BLOCK) void k_update(Params P) {
+    DevState* st = P.st;
+    if (stopped(st)) return;
+    constexpr int WAVES = BLOCK / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // entering column: MINLOC over all ranks' candidates (v4:294-302)
+    double min_e = INFINITY;
+    int64_t p = INT64_MAX;
+    for (int g = 0; g < P.nin; ++g) {
+        const ArgMinEntry e = P.price_in[g];
+        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
+    }
+    if (min_e >= -P.eps || p == INT64_MAX) {  // OptimumFound (v4:299-302)
+        if (blockIdx.x == 0 && tid == 0) {
+            st->p = p;
+            st->min_e = min_e;
+            st->status = ST_OPTIMAL;
+        }
+        return;
+    }
+
+    const int64_t it = st->iter;
+    const int par = (int)(it & 1);
+    const int64_t m = P.m, L = P.L, L2 = L >> 1;
+    const dbl2* __restrict__ src = reinterpret_cast<const dbl2*>(par ? P.B1 : P.B0);
+    dbl2* __restrict__ dst = reinterpret_cast<dbl2*>(par ? P.B0 : P.B1);
+    const double* Ep = par ? P.E1 : P.E0;
+    const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(par ? P.r1 : P.r0);
+    const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
+
+    const int64_t row0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
+    const int nvalid = (int)((row0 >= m) ? 0 : ((m - row0 < R) ? (m - row0) : R));
+    double ei[R], acc[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        ei[u] = (u < nvalid) ? Ep[row0 + u] : 0.0;
+        acc[u] = 0.0;
+    }
+    const int64_t base = row0 * L2;
+    if (nvalid == R) {
+        constexpr int U = (R >= 4) ? 2 : 4;
+        int64_t k = lane;
+        for (; k + (U - 1) * 64 < L2; k += U * 64) {
+            dbl2 rv[U], av[U], bv[U][R];
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                rv[t] = rp[k + t * 64];
+                av[t] = ap[k + t * 64];
+#pragma unroll
+                for (int u = 0; u < R; ++u) bv[t][u] = __builtin_nontemporal_load(&src[base + u * L2 + k + t * 64]);
+            }
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    dbl2 nv;
+                    nv.x = fma(ei[u], rv[t].x, bv[t][u].x);
+                    nv.y = fma(ei[u], rv[t].y, bv[t][u].y);
+                    __builtin_nontemporal_store(nv, &dst[base + u * L2 + k + t * 64]);
+                    acc[u] = fma(nv.x, av[t].x, acc[u]);
+                    acc[u] = fma(nv.y, av[t].y, acc[u]);
+                }
+            }
+        }
+        for (; k < L2; k += 64) {
+            const dbl2 rv = rp[k], av = ap[k];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const dbl2 bv = src[base + u * L2 + k];
+                dbl2 nv;
+                nv.x = fma(ei[u], rv.x, bv.x);
+                nv.y = fma(ei[u], rv.y, bv.y);
+                dst[base + u * L2 + k] = nv;
+                acc[u] = fma(nv.x, av.x, acc[u]);
+                acc[u] = fma(nv.y, av.y, acc[u]);
+            }
+        }
+    } else if (nvalid > 0) {
+        for (int64_t k = lane; k < L2; k += 64) {
+            const dbl2 rv = rp[k], av = ap[k];
+            for (int u = 0; u < nvalid; ++u) {
+                const dbl2 bv = src[base + u * L2 + k];
+                dbl2 nv;
+                nv.x = fma(ei[u], rv.x, bv.x);
+                nv.y = fma(ei[u], rv.y, bv.y);
+                dst[base + u * L2 + k] = nv;
+                acc[u] = fma(nv.x, av.x, acc[u]);
+                acc[u] = fma(nv.y, av.y, acc[u]);
+            }
+        }
+    }
+
+    // alpha_i, theta_i (compute_theta, v4:199-208) and the wave's argmin
+    double wbest = INFINITY;
+    int64_t wi = INT64_MAX;
+    int64_t nonpos = 0;
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        if (u < nvalid) {
+            const double a = wave_sum(acc[u]);
+            const int64_t i = row0 + u;
+            if (lane == 0) st_agent(&P.alpha[i], a);
+            const bool pos = a > 0.0;
+            const double th = pos ? P.x_b[i] / a : INFINITY;
+            nonpos += !pos;
+            if (argmin_better(th, i, wbest, wi)) { wbest = th; wi = i; }
+        }
+    }
+    drain_vmem();  // every storing wave drains its alpha stores before the barrier
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
+    int* s_last = reinterpret_cast<int*>(smem + sizeof(UpdPartial) * BLOCK);
+    if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, 0};
+    __syncthreads();
+    if (tid == 0) {
+        UpdPartial w = red[0];
+        for (int i = 1; i < WAVES; ++i) {
+            if (argmin_better(red[i].theta, red[i].idx, w.theta, w.idx)) { w.theta = red[i].theta; w.idx = red[i].idx; }
+            w.nonpos += red[i].nonpos;
+        }
+        st_agent(&P.upd_partials[blockIdx.x].theta, w.theta);
+        st_agent(&P.upd_partials[blockIdx.x].idx, w.idx);
+        st_agent(&P.upd_partials[blockIdx.x].nonpos, w.nonpos);
+        drain_vmem();
+        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = (t == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    update_tail<BLOCK>(P, st, p, min_e, it, par, smem);
+}
+
+// ---------------------------------------------------------------------------
+// Setup / readback kernels (off the hot loop)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double uniform01(uint64_t seed, uint64_t stream, uint64_t idx) {
+    const uint64_t key = (seed * 0x9E3779B97F4A7C15ULL) ^ (stream << 56) ^ idx;
+    return (double)(splitmix64(key) >> 11) * 0x1.0p-53;
+}
+
+__global__ void k_generate(double* A, double* b, double* c, int64_t m, int64_t n, int64_t L,
+                           uint64_t seed) {
+    const int64_t ns = n - m;
+    const int64_t total = L * n;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = t / L, i = t - j * L;
+        double v = 0.0;
+        if (i < m) v = (j < ns) ? uniform01(seed, 1, (uint64_t)(i + j * m)) : ((i == j - ns) ? 1.0 : 0.0);
+        A[t] = v;
+        if (j == 0) b[i] = (i < m) ? ((double)ns / 4.0) * (1.0 + uniform01(seed, 2, (uint64_t)i)) : 0.0;
+        if (i == 0) c[j] = (j < ns) ? uniform01(seed, 3, (uint64_t)j) : 0.0;
+    }
+}
+
+// slack basis (v4:268-277 with the intended semantics)
+__global__ void k_reset(Params P) {
+    const int64_t m = P.m, n = P.n, L = P.L, ns = P.ns;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < m; i += stride) {
+        P.B0[i * L + i] = 1.0;  // init_I (v4:182-188); buffers zeroed by the host
+        P.c_B[i] = P.c[ns + i];
+        P.x_b[i] = P.b[i];
+        P.y[i] = P.c[ns + i];
+        P.b_ixs[i] = ns + i;
+    }
+    for (int64_t j = t0; j < n; j += stride) {
+        int32_t pos = -1;
+        if (j < ns && j >= P.s_lo && j < P.s_hi) {
+            pos = (int32_t)(j - P.s_lo);
+            P.nb_list[pos] = (int32_t)j;
+        }
+        P.nb_pos[j] = pos;
+    }
+    if (t0 == 0) {
+        DevState* st = P.st;
+        st->status = ST_RUNNING;
+        st->nb_count = (int32_t)(P.s_hi - P.s_lo);
+        st->iter = 0;
+        st->limit = 0;
+        st->p = -1;
+        st->q = -1;
+        st->min_e = 0.0;
+        st->z = 0.0;
+        st->ticket_price = 0;
+        st->ticket_update = 0;
+    }
+    (void)L;
+}
+
+// B^-1 with the pending update applied, into out (m x L row-major)
+__global__ void k_materialize(Params P, double* out) {
+    const DevState* st = P.st;
+    const int par = (int)(st->iter & 1);
+    const double* B = par ? P.B1 : P.B0;
+    const double* E = par ? P.E1 : P.E0;
+    const double* r = par ? P.r1 : P.r0;
+    const int64_t total = P.m * P.L;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / P.L, k = t - i * P.L;
+        out[t] = fma(E[i], r[k], B[t]);
+    }
+}
+
+// e_j for every column (debug / parity), one wave per column
+__global__ __launch_bounds__(256) void k_reduced_costs(Params P, double* e) {
+    const int lane = threadIdx.x & 63;
+    const int64_t L2 = P.L >> 1;
+    const dbl2* y2 = reinterpret_cast<const dbl2*>(P.y);
+    for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < P.n;
+         j += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const dbl2* col = reinterpret_cast<const dbl2*>(P.A + j * P.L);
+        double a0 = 0.0, a1 = 0.0;
+        for (int64_t k = lane; k < L2; k += 64) {
+            const dbl2 v = col[k], w = y2[k];
+            a0 = fma(v.x, w.x, a0);
+            a1 = fma(v.y, w.y, a1);
+        }
+        const double s = wave_sum(a0 + a1) - P.c[j];
+        if (lane == 0) e[j] = s;
+    }
+}
+
+// z = c_B . x_b (v4:365)
+__global__ __launch_bounds__(256) void k_objective(Params P) {
+    __shared__ double sa[256], sb[256];
+    double s = 0.0, d = 0.0;
+    for (int64_t i = threadIdx.x; i < P.m; i += 256) s = fma(P.c_B[i], P.x_b[i], s);
+    block_sum2<256>(s, d, sa, sb);
+    if (threadIdx.x == 0) P.st->z = s;
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers
+// ---------------------------------------------------------------------------
+template <int BLOCK, bool LDS_Y>
+static hipError_t launch_price_t(const Params& P, int grid, size_t lds, hipStream_t s,
+                                 hipEvent_t e0, hipEvent_t e1) {
+    if (e0 || e1) {
+        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1,
+                              0, P);
+    } else {
+        hipLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), lds, s, P);
+    }
+    return hipGetLastError();
+}
+
+template <int BLOCK, bool LDS_Y>
+static hipError_t prep_price_t(size_t lds, int* blocks_per_cu) {
+    hipError_t e = hipSuccess;
+    if (lds > 65536) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_price<BLOCK, LDS_Y>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_price<BLOCK, LDS_Y>, BLOCK, lds);
+}
+
+hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu) {
+    if (c.lds_y) {
+        switch (c.block) {
+            case 256: return prep_price_t<256, true>(c.lds_bytes, blocks_per_cu);
+            case 512: return prep_price_t<512, true>(c.lds_bytes, blocks_per_cu);
+            case 1024: return prep_price_t<1024, true>(c.lds_bytes, blocks_per_cu);
+        }
+    } else {
+        switch (c.block) {
+            case 256: return prep_price_t<256, false>(c.lds_bytes, blocks_per_cu);
+            case 512: return prep_price_t<512, false>(c.lds_bytes, blocks_per_cu);
+            case 1024: return prep_price_t<1024, false>(c.lds_bytes, blocks_per_cu);
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (c.lds_y) {
+        switch (c.block) {
+            case 256: return launch_price_t<256, true>(P, c.grid, c.lds_bytes, s, e0, e1);
+            case 512: return launch_price_t<512, true>(P, c.grid, c.lds_bytes, s, e0, e1);
+            case 1024: return launch_price_t<1024, true>(P, c.grid, c.lds_bytes, s, e0, e1);
+        }
+    } else {
+        switch (c.block) {
+            case 256: return launch_price_t<256, false>(P, c.grid, c.lds_bytes, s, e0, e1);
+            case 512: return launch_price_t<512, false>(P, c.grid, c.lds_bytes, s, e0, e1);
+            case 1024: return launch_price_t<1024, false>(P, c.grid, c.lds_bytes, s, e0, e1);
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int R>
+static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    constexpr int BLOCK = 256;
+    const size_t lds = sizeof(UpdPartial) * BLOCK + 16;
+    if (e0 || e1) {
+        hipExtLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+    } else {
+        hipLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), lds, s, P);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    switch (c.rows) {
+        case 1: return launch_update_t<1>(P, c.grid, s, e0, e1);
+        case 2: return launch_update_t<2>(P, c.grid, s, e0, e1);
+        case 4: return launch_update_t<4>(P, c.grid, s, e0, e1);
+        case 8: return launch_update_t<8>(P, c.grid, s, e0, e1);
+    }
+    return hipErrorInvalidValue;
+}
+
+static int grid_for(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n, int64_t L, uint64_t seed,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_generate, dim3(grid_for(L * n, 256) * 4), dim3(256), 0, s, A, b, c, m, n, L, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_reset(const Params& P, hipStream_t s) {
+    const int64_t w = P.m > P.n ? P.m : P.n;
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(w, 256)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_materialize(const Params& P, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_materialize, dim3(grid_for(P.m * P.L, 256)), dim3(256), 0, s, P, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s) {
+    hipLaunchKernelGGL(k_reduced_costs, dim3(grid_for(P.n * 64, 256)), dim3(256), 0, s, P, e);
+    return hipGetLastError();
+}
+
+hipError_t launch_objective(const Params& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_objective, dim3(1), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+}  // namespace spx
