@@ -71,10 +71,12 @@ typedef struct spx_opts {
     int32_t update_rows;  /* tuning: B^-1 rows per wave in the update, 0 = auto */
     int32_t price_grid;   /* tuning: pricing workgroups, 0 = auto              */
     int32_t flags;        /* SPX_FLAG_* bits                                   */
-    int32_t reserved[6];
+    int32_t update_block; /* tuning: threads per update workgroup, 0 = auto    */
+    int32_t reserved[5];
 } spx_opts;
 
-#define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times) */
+#define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times)  */
+#define SPX_FLAG_STAMPS 2 /* in-kernel phase stamps (spx_phase_times); diagnostic */
 
 void spx_default_opts(spx_opts* opts);
 
@@ -137,6 +139,15 @@ int spx_objective(spx_ctx* ctx, double* z);
  * pricing kernel and of the fused update kernel since the last call (resets). */
 int spx_kernel_times(spx_ctx* ctx, double* price_ms, int64_t* price_launches,
                      double* update_ms, int64_t* update_launches);
+
+/* With SPX_FLAG_STAMPS: microseconds summed since the last call of, per
+ * kernel, the body (earliest workgroup start -> last workgroup's ticket) and
+ * the last-workgroup tail (final reduction; for the update kernel also E_q,
+ * r, x_b, y and the basis bookkeeping).  out[0..3] = price body, price tail,
+ * update body, update tail; out[4..8] = update-tail sub-phases (partials ->
+ * q, row-q loads + E/r/dots, block sum, x_b/y stores, bookkeeping).  Resets. */
+#define SPX_PHASES 9
+int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
 /* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this
  * rank (8*(m+1)*local non-basic columns), bytes_update: one update launch

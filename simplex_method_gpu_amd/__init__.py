@@ -27,6 +27,7 @@ __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_un
            "SimplexError", "FLAG_TIMING"]
 
 FLAG_TIMING = 1
+FLAG_STAMPS = 2
 
 
 class SolveStatus(IntEnum):
@@ -99,13 +100,14 @@ class Context:
     def __init__(self, A_cols=None, b=None, c=None, *, m: int | None = None, n: int | None = None,
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
-                 update_rows: int = 0, price_grid: int = 0):
+                 update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
         o.eps, o.device, o.rank, o.nranks = eps, device, rank, nranks
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
-        o.flags = FLAG_TIMING if timing else 0
+        o.update_block = update_block
+        o.flags = (FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
@@ -201,6 +203,15 @@ class Context:
                                        ctypes.byref(nu)))
         return {"price_ms": tp.value, "price_launches": np_.value,
                 "update_ms": tu.value, "update_launches": nu.value}
+
+    def phase_times(self):
+        """In-kernel phase split (needs stamps=True), microseconds summed."""
+        out = (ctypes.c_double * 9)()
+        check(self._L.spx_phase_times(self._h, out))
+        return {"price_body_us": out[0], "price_tail_us": out[1],
+                "update_body_us": out[2], "update_tail_us": out[3],
+                "tail_partials_us": out[4], "tail_rowq_us": out[5], "tail_blocksum_us": out[6],
+                "tail_stores_us": out[7], "tail_bookkeeping_us": out[8]}
 
     def info(self):
         m, n, ld, nb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

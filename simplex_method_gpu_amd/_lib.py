@@ -27,7 +27,8 @@ class SpxOpts(ctypes.Structure):
         ("update_rows", ctypes.c_int32),
         ("price_grid", ctypes.c_int32),
         ("flags", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 6),
+        ("update_block", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 5),
     ]
 
 
@@ -48,6 +49,7 @@ SIGNATURES = {
     "spx_objective": (ctypes.c_int, [_p, _p]),
     "spx_kernel_times": (ctypes.c_int, [_p, _p, _p, _p, _p]),
     "spx_info": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p]),
+    "spx_phase_times": (ctypes.c_int, [_p, _p]),
     "spx_shard_range": (ctypes.c_int, [_i64, _i64, _i32, _i32, _p]),
     "spx_minloc_merge": (ctypes.c_int, [_p, _p, _i32, _p, _p]),
     "spx_last_error": (ctypes.c_char_p, []),

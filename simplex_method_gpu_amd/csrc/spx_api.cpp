@@ -229,7 +229,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (x->opts.price_block == 256 || x->opts.price_block == 512 || x->opts.price_block == 1024)
         pc.block = x->opts.price_block;
     else
-        pc.block = ybytes <= 40 * 1024 ? 256 : (ybytes <= 72 * 1024 ? 512 : 1024);
+        pc.block = ybytes <= 72 * 1024 ? 512 : 1024;
     pc.lds_y = ybytes + (size_t)pc.block * 16 + 16 <= 150 * 1024;
     pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (size_t)pc.block * sizeof(ArgMinEntry) + 16;
     int per_cu = 0;
@@ -242,13 +242,23 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (x->opts.price_grid > 0) pc.grid = x->opts.price_grid;
 
     UpdateCfg& uc = x->ucfg;
+    int ub = x->opts.update_block;
+    if (!(ub == 256 || ub == 512 || ub == 1024)) ub = 1024;
     int rows = x->opts.update_rows;
-    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = (m >= 8192) ? 4 : (m >= 2048 ? 2 : 1);
+    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = 1;
+    if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
+    uc.block = ub;
     uc.rows = rows;
-    uc.grid = (int)std::max<int64_t>(1, (m + 4 * rows - 1) / (4 * rows));
+    const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
+    uc.grid = (int)std::max<int64_t>(1, (m + rows_per_wg - 1) / rows_per_wg);
 
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
+    if (x->opts.flags & SPX_FLAG_STAMPS) {
+        SPX_TRY(x->alloc(&P.stamps, 16));
+        const unsigned long long init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
+        HIP_TRY(hipMemcpy(P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
+    }
     SPX_TRY(x->alloc(&x->send, 1));
     SPX_TRY(x->alloc(&x->recv, (size_t)G));
     P.price_out = x->send;
@@ -568,6 +578,23 @@ int spx_kernel_times(spx_ctx* x, double* price_ms, int64_t* np, double* update_m
     if (np) *np = (int64_t)x->n_price;
     if (nu) *nu = (int64_t)x->n_update;
     x->n_price = x->n_update = 0;
+    return SPX_OK;
+}
+
+int spx_phase_times(spx_ctx* x, double out[SPX_PHASES]) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
+    unsigned long long h[16];
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(h, x->P.stamps, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 5; ++k) out[4 + k] = h[8 + k] * 0.01;
+    HIP_TRY(hipMemset(x->P.stamps + 8, 0, 8 * sizeof(unsigned long long)));
+    out[0] = h[1] * 0.01;  // 100 MHz ticks -> us
+    out[1] = h[2] * 0.01;
+    out[2] = h[5] * 0.01;
+    out[3] = h[6] * 0.01;
+    const unsigned long long init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
+    HIP_TRY(hipMemcpy(x->P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
     return SPX_OK;
 }
 

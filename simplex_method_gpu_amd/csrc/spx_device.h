@@ -84,6 +84,9 @@ struct Params {
     int32_t nin;
     UpdPartial* upd_partials;
     DevState* st;
+    // diagnostics (SPX_FLAG_STAMPS): per kernel {min WG start, sum body, sum tail}
+    // in s_memrealtime ticks (100 MHz); nullptr in normal runs
+    unsigned long long* stamps;
 };
 
 __host__ __device__ inline bool owns_col(const Params& P, int64_t j) {

@@ -14,8 +14,9 @@ struct PriceCfg {
 };
 
 struct UpdateCfg {
-    int rows;  // B^-1 rows per wave (1/2/4/8); block is 256 threads
-    int grid;  // ceil(m / (4 * rows))
+    int block;  // threads per workgroup (256 / 512 / 1024)
+    int rows;   // B^-1 rows per wave (1/2/4/8)
+    int grid;   // ceil(m / (block / 64 * rows))
 };
 
 hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu);

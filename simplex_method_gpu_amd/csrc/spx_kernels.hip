@@ -49,6 +49,31 @@ __device__ __forceinline__ bool stopped(const DevState* st) {
     return st->status != ST_RUNNING || st->iter >= st->limit;
 }
 
+// Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
+// launch, slot[1] += (last-workgroup ticket - start), slot[2] += tail duration.
+__device__ __forceinline__ unsigned long long rtime() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_start(unsigned long long* slot) {
+    if (slot && threadIdx.x == 0) atomicMin(&slot[0], rtime());
+}
+__device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned long long t_tail) {
+    if (slot && threadIdx.x == 0) {
+        const unsigned long long t_end = rtime();
+        const unsigned long long t0 = __hip_atomic_load(&slot[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&slot[1], t_tail - t0);
+        atomicAdd(&slot[2], t_end - t_tail);
+        __hip_atomic_store(&slot[0], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Diagnostic sub-phase marks inside the update tail: slot 8+k accumulates the
+// ticks since the previous mark (thread 0 only).
+__device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, unsigned long long prev) {
+    if (!P.stamps || threadIdx.x != 0) return prev;
+    const unsigned long long now = rtime();
+    atomicAdd(&P.stamps[8 + k], now - prev);
+    return now;
+}
+
 // ---------------------------------------------------------------------------
 // Pricing + entering argmin
 // ---------------------------------------------------------------------------
@@ -56,6 +81,8 @@ template <int BLOCK, bool LDS_Y>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
     if (stopped(st)) return;
+    unsigned long long* const slot = P.stamps;
+    stamp_start(slot);
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t L = P.L;
@@ -121,6 +148,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     }
     __syncthreads();
     if (!*s_last) return;
+    const unsigned long long t_tail = slot ? rtime() : 0;
 
     // last workgroup: reduce all partials
     ArgMinEntry w{INFINITY, INT64_MAX};
@@ -140,39 +168,42 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         *P.price_out = red[0];
         st_agent(&st->ticket_price, 0u);
     }
+    stamp_tail(slot, t_tail);
 }
 
 // ---------------------------------------------------------------------------
 // Fused: pending rank-1 update + FTRAN + ratio test + leaving argmin + tail
 // ---------------------------------------------------------------------------
+// Block-wide sum of two doubles: wave butterflies, then one LDS pass over the
+// per-wave sums in wave order (deterministic for a fixed BLOCK).
 template <int BLOCK>
 __device__ void block_sum2(double& a, double& b, double* sa, double* sb) {
-    const int tid = threadIdx.x;
-    sa[tid] = a;
-    sb[tid] = b;
-    __syncthreads();
-    for (int s = BLOCK / 2; s > 0; s >>= 1) {
-        if (tid < s) {
-            sa[tid] += sa[tid + s];
-            sb[tid] += sb[tid + s];
-        }
-        __syncthreads();
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+        sa[wave] = a;
+        sb[wave] = b;
     }
-    a = sa[0];
-    b = sb[0];
+    __syncthreads();
+    double ta = sa[0], tb = sb[0];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) {
+        ta += sa[w];
+        tb += sb[w];
+    }
+    a = ta;
+    b = tb;
     __syncthreads();
 }
 
-// Runs in the last workgroup of k_update: everything after the leaving argmin
-// (v4:317-357) on O(m) vectors.
+// Leaving argmin over the k_update workgroup partials + unbounded count
+// (v4:317-325).  Result broadcast to every thread.
 template <int BLOCK>
-__device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            int par, unsigned char* smem) {
-    const int tid = threadIdx.x;
-    const int64_t m = P.m, L = P.L;
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
-
-    // (1) leaving argmin over workgroup partials + unbounded count (v4:317-325)
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red) {
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     UpdPartial w{INFINITY, INT64_MAX, 0, 0};
     for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
         const double th = ld_agent(&P.upd_partials[g].theta);
@@ -181,34 +212,78 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
         if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
         w.nonpos += np;
     }
-    red[tid] = w;
-    __syncthreads();
-    for (int s = BLOCK / 2; s > 0; s >>= 1) {
-        if (tid < s) {
-            UpdPartial a = red[tid];
-            const UpdPartial bq = red[tid + s];
-            if (argmin_better(bq.theta, bq.idx, a.theta, a.idx)) { a.theta = bq.theta; a.idx = bq.idx; }
-            a.nonpos += bq.nonpos;
-            red[tid] = a;
-        }
-        __syncthreads();
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double th = __shfl_xor(w.theta, off, 64);
+        const int64_t i = __shfl_xor(w.idx, off, 64);
+        w.nonpos += __shfl_xor(w.nonpos, off, 64);
+        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
     }
-    const int64_t q = red[0].idx;
-    const int64_t nonpos = red[0].nonpos;
+    if (lane == 0) red[wave] = w;
     __syncthreads();
-    // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no valid
-    // candidate at all (NaN-poisoned x_b) stops the same way instead of
-    // indexing out of range.
-    if (nonpos == m || q < 0 || q >= m) {
-        if (tid == 0) {
-            st->p = p;
-            st->min_e = min_e;
-            st->q = -1;
-            st->status = ST_UNBOUNDED;
-            st_agent(&st->ticket_update, 0u);
-        }
-        return;
+    UpdPartial t = red[0];
+#pragma unroll
+    for (int k = 1; k < WAVES; ++k) {
+        if (argmin_better(red[k].theta, red[k].idx, t.theta, t.idx)) { t.theta = red[k].theta; t.idx = red[k].idx; }
+        t.nonpos += red[k].nonpos;
     }
+    __syncthreads();
+    return t;
+}
+
+struct TailShared {
+    double aq, eq, c_bq;
+    int64_t leave;
+};
+
+// Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and the
+// loop counters; thread 0 only, after every other use of c_B / b_ixs.
+__device__ __forceinline__ void tail_bookkeeping(const Params& P, DevState* st, int64_t p, int64_t q, double c_p,
+                                                 int64_t leave, int cnt, int kp, int last, bool own_p,
+                                                 double min_e, int64_t it) {
+    P.c_B[q] = c_p;
+    P.b_ixs[q] = p;
+    if (own_p) {
+        P.nb_list[kp] = last;
+        P.nb_pos[last] = kp;
+        P.nb_pos[p] = -1;
+        --cnt;
+    }
+    if (owns_col(P, leave)) {
+        P.nb_list[cnt] = (int32_t)leave;
+        P.nb_pos[leave] = cnt;
+        ++cnt;
+    }
+    st->nb_count = cnt;
+    st->p = p;
+    st->q = q;
+    st->min_e = min_e;
+    st->iter = it + 1;
+    st_agent(&st->ticket_update, 0u);
+}
+
+__device__ __forceinline__ void tail_unbounded(DevState* st, int64_t p, double min_e) {
+    st->p = p;
+    st->min_e = min_e;
+    st->q = -1;
+    st->status = ST_UNBOUNDED;
+    st_agent(&st->ticket_update, 0u);
+}
+
+// Runs in the last workgroup of k_update: everything after the leaving argmin
+// (v4:317-357) on O(m) vectors.  Latency-bound (one workgroup, the rest of the
+// GPU idle), so it is built around two dependent memory round trips: the
+// inputs that do not depend on q (alpha, c_B, b, r_prev and the list words of
+// p) are loaded before the partial reduction that yields q; B_old[q,:], x_b, y
+// and row q's scalars are loaded together right after it.
+// Needs m <= CH * BLOCK (one element chunk per thread held in registers).
+template <int BLOCK, int CH>
+__device__ void update_tail_regs(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
+                                 unsigned char* smem) {
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x;
+    const int64_t m = P.m, L = P.L;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
 
     const double* Bsrc = par ? P.B1 : P.B0;
     const double* Ep = par ? P.E1 : P.E0;
@@ -216,66 +291,201 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
     double* Ec = par ? P.E0 : P.E1;
     double* rc = par ? P.r0 : P.r1;
 
-    // (2) E_q (compute_E_q, v4:210-215)
-    const double aq = ld_agent(&P.alpha[q]);
-    for (int64_t i = tid; i < m; i += BLOCK) {
-        const double a = ld_agent(&P.alpha[i]);
-        Ec[i] = (i != q) ? (-a / aq) : (1.0 / aq - 1.0);
+    // round trip 1 (overlaps the partial loads): everything independent of q
+    double a[CH], cb[CH], bb[CH], rr[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int64_t i = (int64_t)u * BLOCK + tid;
+        if (i < m) {
+            a[u] = ld_agent(&P.alpha[i]);
+            cb[u] = P.c_B[i];
+            bb[u] = P.b[i];
+            rr[u] = rp[i];
+        }
     }
-    // (3) pivot row r = B^-1_new[q,:] (v4:331), recomputed exactly as the
-    //     streaming pass wrote it: fma(E_prev[q], r_prev[k], B_old[q,k])
-    const double eq = Ep[q];
-    const double* brow = Bsrc + q * L;
-    for (int64_t k = tid; k < L; k += BLOCK) rc[k] = fma(eq, rp[k], brow[k]);
-
-    // (4) s_x = r.b (v4:347), s_y = c_B_new.E_q (v4:354), c_B_new[q] = c_p
     const double c_p = P.c[p];
-    double sx = 0.0, sy = 0.0;
-    for (int64_t k = tid; k < m; k += BLOCK) sx = fma(rc[k], P.b[k], sx);
-    for (int64_t i = tid; i < m; i += BLOCK) sy = fma((i == q) ? c_p : P.c_B[i], Ec[i], sy);
-    double* sa = reinterpret_cast<double*>(smem);
-    double* sb = sa + BLOCK;
-    block_sum2<BLOCK>(sx, sy, sa, sb);
-    const double c_bq = P.c_B[q];
-    const double s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
-
-    // (5) x_b += s_x E_q (v4:348); y += s_y r (v4:356)
-    for (int64_t i = tid; i < m; i += BLOCK) P.x_b[i] = fma(sx, Ec[i], P.x_b[i]);
-    for (int64_t k = tid; k < m; k += BLOCK) P.y[k] = fma(s_y, rc[k], P.y[k]);
-    __syncthreads();
-
-    // (6) basis bookkeeping (v4:339-342) + non-basic list
+    const bool own_p = owns_col(P, p);
+    int cnt = 0, kp = -1, last = -1;
     if (tid == 0) {
-        const int64_t leave = P.b_ixs[q];
-        P.c_B[q] = c_p;
-        P.b_ixs[q] = p;
-        int cnt = st->nb_count;
-        if (owns_col(P, p)) {
-            const int kp = P.nb_pos[p];
-            const int last = P.nb_list[cnt - 1];
-            P.nb_list[kp] = last;
-            P.nb_pos[last] = kp;
-            P.nb_pos[p] = -1;
-            --cnt;
+        cnt = st->nb_count;
+        if (own_p) {
+            kp = P.nb_pos[p];
+            last = P.nb_list[cnt - 1];
         }
-        if (owns_col(P, leave)) {
-            P.nb_list[cnt] = (int32_t)leave;
-            P.nb_pos[leave] = cnt;
-            ++cnt;
-        }
-        st->nb_count = cnt;
-        st->p = p;
-        st->q = q;
-        st->min_e = min_e;
-        st->iter = it + 1;
-        st_agent(&st->ticket_update, 0u);
     }
+
+    unsigned long long tm = P.stamps ? rtime() : 0;
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
+    tm = tail_mark(P, 0, tm);
+    const int64_t q = t.idx;
+    if (t.nonpos == m || q < 0 || q >= m) {  // Unbounded (v4:319-322)
+        if (tid == 0) tail_unbounded(st, p, min_e);
+        return;
+    }
+
+    // round trip 2: row q of B_old, x_b, y and row q's scalars
+    const double* brow = Bsrc + q * L;
+    double br[CH], xv[CH], yv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int64_t i = (int64_t)u * BLOCK + tid;
+        if (i < m) {
+            br[u] = brow[i];
+            xv[u] = P.x_b[i];
+            yv[u] = P.y[i];
+        }
+    }
+    const double aq = ld_agent(&P.alpha[q]);
+    const double eq = Ep[q];
+    const double c_bq = P.c_B[q];
+    int64_t leave = 0;
+    if (tid == 0) leave = P.b_ixs[q];
+
+    // E_q (compute_E_q, v4:210-215); r = B^-1_new[q,:] (v4:331) exactly as the
+    // streaming pass wrote it; s_x = r.b (v4:347); s_y = c_B_new.E_q (v4:354)
+    double sx = 0.0, sy = 0.0;
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int64_t i = (int64_t)u * BLOCK + tid;
+        if (i < m) {
+            a[u] = (i != q) ? (-a[u] / aq) : (1.0 / aq - 1.0);  // a[] now holds E_q
+            rr[u] = fma(eq, rr[u], br[u]);                       // rr[] now holds r
+            sx = fma(rr[u], bb[u], sx);
+            sy = fma((i == q) ? c_p : cb[u], a[u], sy);
+        }
+    }
+    tm = tail_mark(P, 1, tm);
+    double* sa = reinterpret_cast<double*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared));
+    double* sb = sa + WAVES;
+    block_sum2<BLOCK>(sx, sy, sa, sb);
+    tm = tail_mark(P, 2, tm);
+    const double s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+    // x_b += s_x E_q (v4:348); y += s_y r (v4:356)
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+        const int64_t i = (int64_t)u * BLOCK + tid;
+        if (i < m) {
+            Ec[i] = a[u];
+            rc[i] = rr[u];
+            P.x_b[i] = fma(sx, a[u], xv[u]);
+            P.y[i] = fma(s_y, rr[u], yv[u]);
+        }
+    }
+    __syncthreads();
+    tm = tail_mark(P, 3, tm);
+    if (tid == 0) tail_bookkeeping(P, st, p, q, c_p, leave, cnt, kp, last, own_p, min_e, it);
+    tm = tail_mark(P, 4, tm);
+}
+
+// General tail for m > CH * BLOCK: the same steps in element chunks.
+template <int BLOCK>
+__device__ void update_tail_loop(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
+                                 unsigned char* smem) {
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int CH = 4;
+    const int tid = threadIdx.x;
+    const int64_t m = P.m, L = P.L;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
+
+    const double c_p = P.c[p];
+    const bool own_p = owns_col(P, p);
+    int cnt = 0, kp = -1, last = -1;
+    if (tid == 0) {
+        cnt = st->nb_count;
+        if (own_p) {
+            kp = P.nb_pos[p];
+            last = P.nb_list[cnt - 1];
+        }
+    }
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
+    const int64_t q = t.idx;
+    if (t.nonpos == m || q < 0 || q >= m) {
+        if (tid == 0) tail_unbounded(st, p, min_e);
+        return;
+    }
+    const double* Bsrc = par ? P.B1 : P.B0;
+    const double* Ep = par ? P.E1 : P.E0;
+    const double* rp = par ? P.r1 : P.r0;
+    double* Ec = par ? P.E0 : P.E1;
+    double* rc = par ? P.r0 : P.r1;
+    const double* brow = Bsrc + q * L;
+    const double aq = ld_agent(&P.alpha[q]);
+    const double eq = Ep[q];
+    const double c_bq = P.c_B[q];
+    const int64_t leave = P.b_ixs[q];
+
+    double sx = 0.0, sy = 0.0;
+    for (int64_t base = 0; base < m; base += (int64_t)CH * BLOCK) {
+        double a[CH], cb[CH], bb[CH], br[CH], rr[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = base + (int64_t)u * BLOCK + tid;
+            if (i < m) {
+                a[u] = ld_agent(&P.alpha[i]);
+                cb[u] = P.c_B[i];
+                bb[u] = P.b[i];
+                br[u] = brow[i];
+                rr[u] = rp[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = base + (int64_t)u * BLOCK + tid;
+            if (i < m) {
+                const double e = (i != q) ? (-a[u] / aq) : (1.0 / aq - 1.0);
+                const double r = fma(eq, rr[u], br[u]);
+                Ec[i] = e;
+                rc[i] = r;
+                sx = fma(r, bb[u], sx);
+                sy = fma((i == q) ? c_p : cb[u], e, sy);
+            }
+        }
+    }
+    double* sa = reinterpret_cast<double*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared));
+    double* sb = sa + WAVES;
+    block_sum2<BLOCK>(sx, sy, sa, sb);
+    const double s_y = sy + (c_p - c_bq);
+    for (int64_t base = 0; base < m; base += (int64_t)CH * BLOCK) {
+        double xv[CH], yv[CH], ev[CH], rv[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = base + (int64_t)u * BLOCK + tid;
+            if (i < m) {
+                xv[u] = P.x_b[i];
+                yv[u] = P.y[i];
+                ev[u] = Ec[i];
+                rv[u] = rc[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = base + (int64_t)u * BLOCK + tid;
+            if (i < m) {
+                P.x_b[i] = fma(sx, ev[u], xv[u]);
+                P.y[i] = fma(s_y, rv[u], yv[u]);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) tail_bookkeeping(P, st, p, q, c_p, leave, cnt, kp, last, own_p, min_e, it);
+}
+
+template <int BLOCK>
+__device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
+                            unsigned char* smem) {
+    constexpr int CH = 4;
+    if (P.m <= (int64_t)CH * BLOCK)
+        update_tail_regs<BLOCK, CH>(P, st, p, min_e, it, par, smem);
+    else
+        update_tail_loop<BLOCK>(P, st, p, min_e, it, par, smem);
 }
 
 template <int BLOCK, int R>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
     if (stopped(st)) return;
+    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
+    stamp_start(slot);
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -387,7 +597,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     }
     drain_vmem();  // every storing wave drains its alpha stores before the barrier
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
-    int* s_last = reinterpret_cast<int*>(smem + sizeof(UpdPartial) * BLOCK);
+    int* s_last = reinterpret_cast<int*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared) + 16 * WAVES);
     if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, 0};
     __syncthreads();
     if (tid == 0) {
@@ -406,7 +616,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     }
     __syncthreads();
     if (!*s_last) return;
+    const unsigned long long t_tail = slot ? rtime() : 0;
     update_tail<BLOCK>(P, st, p, min_e, it, par, smem);
+    stamp_tail(slot, t_tail);
 }
 
 // ---------------------------------------------------------------------------
@@ -577,10 +789,9 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
     return hipErrorInvalidValue;
 }
 
-template <int R>
+template <int BLOCK, int R>
 static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    constexpr int BLOCK = 256;
-    const size_t lds = sizeof(UpdPartial) * BLOCK + 16;
+    const size_t lds = sizeof(UpdPartial) * (BLOCK / 64) + sizeof(TailShared) + 16 * (BLOCK / 64) + 16;
     if (e0 || e1) {
         hipExtLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
@@ -589,12 +800,24 @@ static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipE
     return hipGetLastError();
 }
 
-hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+template <int BLOCK>
+static hipError_t launch_update_b(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (c.rows) {
-        case 1: return launch_update_t<1>(P, c.grid, s, e0, e1);
-        case 2: return launch_update_t<2>(P, c.grid, s, e0, e1);
-        case 4: return launch_update_t<4>(P, c.grid, s, e0, e1);
-        case 8: return launch_update_t<8>(P, c.grid, s, e0, e1);
+        case 1: return launch_update_t<BLOCK, 1>(P, c.grid, s, e0, e1);
+        case 2: return launch_update_t<BLOCK, 2>(P, c.grid, s, e0, e1);
+        case 4: return launch_update_t<BLOCK, 4>(P, c.grid, s, e0, e1);
+        case 8:
+            if constexpr (BLOCK <= 512) return launch_update_t<BLOCK, 8>(P, c.grid, s, e0, e1);
+            break;
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    switch (c.block) {
+        case 256: return launch_update_b<256>(P, c, s, e0, e1);
+        case 512: return launch_update_b<512>(P, c, s, e0, e1);
+        case 1024: return launch_update_b<1024>(P, c, s, e0, e1);
     }
     return hipErrorInvalidValue;
 }
