@@ -97,6 +97,14 @@ void spx_destroy(spx_ctx* ctx);
 int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]);
 int spx_attach_comm(spx_ctx* ctx, const uint8_t id[SPX_COMM_ID_BYTES]);
 
+/* In-process shard group: G contexts created with nranks = G and ranks
+ * 0..G-1 (any devices, no communicator) run k lockstep iterations with the
+ * MINLOC candidates exchanged by device-to-device copies instead of RCCL
+ * (one host thread drives all shards; single-process multi-GPU, and the
+ * way the sharded path is validated on one GPU).  status/pivots: rank 0's. */
+int spx_group_iterate(spx_ctx** ctxs, int32_t G, int64_t k, int32_t* status,
+                      int64_t* pivots);
+
 /* Back to the slack basis (keeps A, b, c). */
 int spx_reset(spx_ctx* ctx);
 

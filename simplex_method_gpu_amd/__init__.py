@@ -23,7 +23,7 @@ import numpy as np
 from ._lib import SimplexError, SpxOpts, check, load
 
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
-           "shard_range", "minloc_merge",
+           "shard_range", "minloc_merge", "group_iterate",
            "SimplexError", "FLAG_TIMING"]
 
 FLAG_TIMING = 1
@@ -85,6 +85,14 @@ def minloc_merge(vals, idx):
     bv, bi = ctypes.c_double(), ctypes.c_int64()
     check(load().spx_minloc_merge(_ptr(v), _ptr(i), len(v), ctypes.byref(bv), ctypes.byref(bi)))
     return bv.value, bi.value
+
+
+def group_iterate(ctxs, k: int):
+    """Lockstep k iterations of an in-process shard group (see spx_group_iterate)."""
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    st, piv = ctypes.c_int32(), ctypes.c_int64()
+    check(load().spx_group_iterate(arr, len(ctxs), k, ctypes.byref(st), ctypes.byref(piv)))
+    return SolveStatus(st.value), piv.value
 
 
 def comm_unique_id() -> bytes:

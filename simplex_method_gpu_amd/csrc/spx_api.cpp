@@ -105,6 +105,9 @@ struct spx_ctx {
     hipGraph_t graph = nullptr;
     int batch = 0;
 
+    // in-process group exchange
+    hipEvent_t ev_sent = nullptr, ev_recv = nullptr;
+
     // per-kernel timing
     bool timing = false;
     std::vector<hipEvent_t> ev_price, ev_update;  // pairs (start, stop)
@@ -266,7 +269,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.nin = G;
 
     int gb = x->opts.graph_batch;
-    if (gb == 0) gb = 16;
+    if (gb == 0) gb = (G > 1) ? -1 : 16;  // RCCL passes are launched eagerly unless asked
     x->batch = (gb < 0 || x->timing) ? 0 : gb;
     return SPX_OK;
 }
@@ -425,6 +428,8 @@ void spx_destroy(spx_ctx* x) {
     if (x->stream) (void)hipStreamSynchronize(x->stream);
     if (x->graph_exec) (void)hipGraphExecDestroy(x->graph_exec);
     if (x->graph) (void)hipGraphDestroy(x->graph);
+    if (x->ev_sent) (void)hipEventDestroy(x->ev_sent);
+    if (x->ev_recv) (void)hipEventDestroy(x->ev_recv);
     for (hipEvent_t e : x->ev_price) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_update) (void)hipEventDestroy(e);
     if (x->comm) (void)ncclCommDestroy(x->comm);
@@ -467,6 +472,65 @@ int spx_iterate(spx_ctx* x, int64_t k, int32_t* status, int64_t* pivots) {
     SPX_TRY(iterate(x, k));
     if (status) *status = x->status;
     if (pivots) *pivots = x->pivots;
+    return SPX_OK;
+}
+
+int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64_t* pivots) {
+    if (!cs || G < 1) return fail(SPX_ERR_ARG, "bad group");
+    for (int g = 0; g < G; ++g) {
+        spx_ctx* x = cs[g];
+        if (!x) return fail(SPX_ERR_ARG, "NULL context in group");
+        if (x->opts.nranks != G || x->opts.rank != g)
+            return fail(SPX_ERR_ARG, "context %d was created with rank %d / nranks %d", g, x->opts.rank, x->opts.nranks);
+        if (x->comm_ready) return fail(SPX_ERR_STATE, "group contexts must not have a communicator");
+        if (x->m != cs[0]->m || x->n != cs[0]->n) return fail(SPX_ERR_ARG, "group shape mismatch");
+        if (x->status != cs[0]->status || x->pivots != cs[0]->pivots) return fail(SPX_ERR_STATE, "group out of step");
+        if (!x->ev_sent) {
+            HIP_TRY(hipSetDevice(x->device));
+            HIP_TRY(hipEventCreateWithFlags(&x->ev_sent, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&x->ev_recv, hipEventDisableTiming));
+        }
+    }
+    if (cs[0]->status == SPX_STATUS_MAX_ITER && k > 0) {
+        for (int g = 0; g < G; ++g) {
+            HIP_TRY(hipSetDevice(cs[g]->device));
+            SPX_TRY(set_limit(cs[g], cs[g]->pivots + k));
+        }
+        for (int64_t it = 0; it < k; ++it) {
+            for (int g = 0; g < G; ++g) {  // pricing on every shard
+                spx_ctx* x = cs[g];
+                HIP_TRY(hipSetDevice(x->device));
+                HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
+                HIP_TRY(hipEventRecord(x->ev_sent, x->stream));
+            }
+            for (int h = 0; h < G; ++h) {  // all-gather of the 16-byte candidates
+                spx_ctx* x = cs[h];
+                HIP_TRY(hipSetDevice(x->device));
+                for (int g = 0; g < G; ++g) {
+                    HIP_TRY(hipStreamWaitEvent(x->stream, cs[g]->ev_sent, 0));
+                    HIP_TRY(hipMemcpyAsync(x->recv + g, cs[g]->send, sizeof(ArgMinEntry), hipMemcpyDefault,
+                                           x->stream));
+                }
+                HIP_TRY(hipEventRecord(x->ev_recv, x->stream));
+            }
+            for (int g = 0; g < G; ++g) {  // replicated fused update; next pricing waits for every reader
+                spx_ctx* x = cs[g];
+                HIP_TRY(hipSetDevice(x->device));
+                HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
+                for (int h = 0; h < G; ++h) HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv, 0));
+            }
+        }
+        for (int g = 0; g < G; ++g) {
+            HIP_TRY(hipSetDevice(cs[g]->device));
+            SPX_TRY(read_state(cs[g]));
+        }
+        for (int g = 1; g < G; ++g)
+            if (cs[g]->status != cs[0]->status || cs[g]->pivots != cs[0]->pivots)
+                return fail(SPX_ERR_STATE, "shard %d diverged (status %d/%d, pivots %lld/%lld)", g, cs[g]->status,
+                            cs[0]->status, (long long)cs[g]->pivots, (long long)cs[0]->pivots);
+    }
+    if (status) *status = cs[0]->status;
+    if (pivots) *pivots = cs[0]->pivots;
     return SPX_OK;
 }
 

@@ -201,3 +201,45 @@ def test_large_headline_properties(spx):
     assert _rel(s["binv"] @ b, s["x_b"]) < 1e-10
     assert abs(z - float(c[s["b_ixs"]] @ s["x_b"])) <= 1e-10 * abs(z)
     assert np.all(s["x_b"] > -1e-9)  # primal feasibility maintained
+
+
+@pytest.mark.parametrize("G,m,n,k", [(2, 300, 1200, 150), (3, 257, 771, 120), (8, 512, 2048, 200), (4, 5, 7, 10)])
+def test_shard_group_matches_single_rank(spx, G, m, n, k):
+    """Column-sharded pricing over G shards + G-way MINLOC merge + replicated
+    update reproduces the single-rank trajectory bit for bit on every shard."""
+    seed = 11
+    with spx.Context(m=m, n=n, seed=seed) as ref:
+        rst, rpiv = ref.iterate(k)
+        rs = ref.state(binv=True)
+        rz = ref.objective()
+    ctxs = [spx.Context(m=m, n=n, seed=seed, rank=g, nranks=G) for g in range(G)]
+    try:
+        st, piv = spx.group_iterate(ctxs, k)
+        assert st == rst and piv == rpiv
+        for c in ctxs:
+            s = c.state(binv=True)
+            assert np.array_equal(s["b_ixs"], rs["b_ixs"])
+            assert np.array_equal(s["x_b"], rs["x_b"])
+            assert np.array_equal(s["y"], rs["y"])
+            assert np.array_equal(s["binv"], rs["binv"])
+            assert c.objective() == rz
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_shard_group_solves_to_golden_optimum(spx, golden):
+    case = [c for c in golden["cases"] if c["m"] == 256][0]
+    G = 4
+    ctxs = [spx.Context(m=case["m"], n=case["n"], seed=case["seed"], rank=g, nranks=G) for g in range(G)]
+    try:
+        st = spx.SolveStatus.MaxIter
+        while st == spx.SolveStatus.MaxIter:
+            st, piv = spx.group_iterate(ctxs, 64)
+        assert st == spx.SolveStatus.OptimumFound and piv == case["oracle_pivots"]
+        r = ctxs[0].solve(0)
+        assert abs(r.z - case["highs_z"]) <= 1e-9 * abs(case["highs_z"])
+        assert sorted(int(j) for j in r.b_ixs) == case["highs_basis"]
+    finally:
+        for c in ctxs:
+            c.close()
