@@ -354,13 +354,15 @@ int iterate(spx_ctx* x, int64_t k) {
     if (x->status != SPX_STATUS_MAX_ITER || k <= 0) return SPX_OK;
     if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
     SPX_TRY(set_limit(x, x->pivots + k));
-    if (x->batch > 0) {
+    // exactly k passes: whole captured batches, then the remainder eagerly
+    int64_t eager = k;
+    if (x->batch > 0 && k >= x->batch) {
         SPX_TRY(build_graph(x));
-        const int64_t reps = (k + x->batch - 1) / x->batch;
+        const int64_t reps = k / x->batch;
         for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
-    } else {
-        for (int64_t i = 0; i < k; ++i) SPX_TRY(enqueue_pass(x, x->timing));
+        eager = k - reps * x->batch;
     }
+    for (int64_t i = 0; i < eager; ++i) SPX_TRY(enqueue_pass(x, x->timing));
     return read_state(x);
 }
 
