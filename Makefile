@@ -37,3 +37,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle
+
+# cache-policy variants for experiments: make variant NT=<A><BLOAD><BSTORE>, e.g. NT=101
+variant:
+	@mkdir -p $(BUILD)/v$(NT)
+	$(HIPCC) $(HIPFLAGS) -DSPX_NT_A=$(word 1,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
+	  -DSPX_NT_BLOAD=$(word 2,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
+	  -DSPX_NT_BSTORE=$(word 3,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
+	  -c $(SRC)/spx_kernels.hip -o $(BUILD)/v$(NT)/spx_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/v$(NT)/libsimplex.so $(BUILD)/v$(NT)/spx_kernels.o $(BUILD)/spx_api.o $(LDFLAGS)

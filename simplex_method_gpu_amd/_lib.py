@@ -9,7 +9,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsimplex.so")
+# SPX_LIB: alternative build of the same library (e.g. a cache-policy variant
+# from tools/policy_sweep.sh); default is the in-tree product build.
+LIB_PATH = os.environ.get("SPX_LIB") or os.path.join(_HERE, "libsimplex.so")
 
 # symbol -> (restype, argtypes); mirrors include/simplex.h
 _d, _i32, _i64, _u64, _p = ctypes.c_double, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p

@@ -204,14 +204,15 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.eps = x->opts.eps;
     SPX_TRY(x->alloc(&P.B0, (size_t)(m * L)));
     SPX_TRY(x->alloc(&P.B1, (size_t)(m * L)));
-    SPX_TRY(x->alloc(&P.E0, (size_t)L));
-    SPX_TRY(x->alloc(&P.E1, (size_t)L));
-    SPX_TRY(x->alloc(&P.r0, (size_t)L));
-    SPX_TRY(x->alloc(&P.r1, (size_t)L));
-    SPX_TRY(x->alloc(&P.y, (size_t)L));
+    SPX_TRY(x->alloc(&P.alpha0, (size_t)L));
+    SPX_TRY(x->alloc(&P.alpha1, (size_t)L));
+    SPX_TRY(x->alloc(&P.y0, (size_t)L));
+    SPX_TRY(x->alloc(&P.y1, (size_t)L));
     SPX_TRY(x->alloc(&P.x_b, (size_t)L));
     SPX_TRY(x->alloc(&P.c_B, (size_t)L));
-    SPX_TRY(x->alloc(&P.alpha, (size_t)L));
+    double* zeros = nullptr;
+    SPX_TRY(x->alloc(&zeros, (size_t)L));
+    P.zeros = zeros;
     SPX_TRY(x->alloc(&P.b_ixs, (size_t)m));
     SPX_TRY(x->alloc(&P.nb_list, (size_t)n));
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
@@ -278,7 +279,7 @@ int do_reset(spx_ctx* x) {
     const size_t mb = (size_t)(x->m * x->L) * sizeof(double);
     HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
     HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
-    for (double* v : {x->P.E0, x->P.E1, x->P.r0, x->P.r1, x->P.y, x->P.x_b, x->P.c_B, x->P.alpha})
+    for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
     HIP_TRY(launch_reset(x->P, x->stream));
     HIP_TRY(hipStreamSynchronize(x->stream));
@@ -341,6 +342,14 @@ int read_state(spx_ctx* x) {
     HIP_TRY(hipStreamSynchronize(x->stream));
     x->pivots = x->st_host->iter;
     x->status = x->st_host->status;  // ST_RUNNING == SPX_STATUS_MAX_ITER
+    return SPX_OK;
+}
+
+// Apply the deferred y / x_b updates of the last pivot (spx_device.h) so the
+// vectors in HBM are current.  Not valid between spx_price and spx_pivot.
+int flush(spx_ctx* x) {
+    if (x->stepped_price) return fail(SPX_ERR_STATE, "state readback between spx_price and spx_pivot");
+    HIP_TRY(launch_flush(x->P, x->stream));
     return SPX_OK;
 }
 
@@ -538,6 +547,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
 
 int spx_objective(spx_ctx* x, double* z) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    SPX_TRY(flush(x));
     HIP_TRY(launch_objective(x->P, x->stream));
     SPX_TRY(read_state(x));
     if (z) *z = x->st_host->z;
@@ -548,9 +558,11 @@ int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_
                   int64_t* pivots) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     const size_t mb = (size_t)x->m * 8;
+    SPX_TRY(flush(x));
+    SPX_TRY(read_state(x));  // y_buf after the flush
     if (x_b) HIP_TRY(hipMemcpyAsync(x_b, x->P.x_b, mb, hipMemcpyDeviceToHost, x->stream));
     if (b_ixs) HIP_TRY(hipMemcpyAsync(b_ixs, x->P.b_ixs, mb, hipMemcpyDeviceToHost, x->stream));
-    if (y) HIP_TRY(hipMemcpyAsync(y, x->P.y, mb, hipMemcpyDeviceToHost, x->stream));
+    if (y) HIP_TRY(hipMemcpyAsync(y, x->st_host->y_buf ? x->P.y1 : x->P.y0, mb, hipMemcpyDeviceToHost, x->stream));
     if (c_b) HIP_TRY(hipMemcpyAsync(c_b, x->P.c_B, mb, hipMemcpyDeviceToHost, x->stream));
     if (binv) {
         double* tmp = nullptr;
@@ -567,6 +579,7 @@ int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_
 
 int spx_reduced_costs(spx_ctx* x, double* e) {
     if (!x || !e) return fail(SPX_ERR_ARG, "NULL argument");
+    SPX_TRY(flush(x));
     double* tmp = nullptr;
     HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)x->n * 8, x->stream));
     HIP_TRY(launch_reduced_costs(x->P, tmp, x->stream));
@@ -620,7 +633,7 @@ int spx_pivot(spx_ctx* x, int64_t* q, int32_t* status) {
     x->stepped_price = false;
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
     SPX_TRY(read_state(x));
-    if (q) *q = x->st_host->q;
+    if (q) *q = (x->status == SPX_STATUS_UNBOUNDED) ? -1 : x->st_host->q;
     if (status) *status = x->status;
     return SPX_OK;
 }

@@ -6,11 +6,22 @@
 //          reference's D = [-c; A] copy (v4:248,278-279) is not built: pricing
 //          reads A and c directly.
 //   B[2]   m x L, ROW-major B^-1 (the reference is column-major, v4:59-60), two
-//          buffers: the update kernel reads B[iter&1] and writes B[(iter+1)&1].
-//          The true inverse is B[iter&1] + E[iter&1] r[iter&1]^T (one rank-1
-//          update is always pending and is applied inside the next FTRAN).
-//   E[2], r[2]  pending eta column and pivot row (L each, padding zero).
-//   y, x_b, c_B, alpha (L each), b_ixs (m int64), b (L), c (n).
+//          buffers: the update kernel of pass `it` reads S = B[it&1] and writes
+//          B[(it+1)&1].
+//
+// Deferred pivot state.  The last pivot (it-1) is kept in factored form and
+// applied by the kernels that stream the data anyway:
+//   true B^-1 = S + E r^T, with r = S[q,:] (row q of S is the new pivot row,
+//          bit-identical to B^-1_new[q,:] of v4:331) and E_i = -alpha_i/alpha_q,
+//          E_q = 1/alpha_q - 1 (compute_E_q, v4:210-215) from alpha[it&1] and the
+//          scalar st->aq — applied by the next k_update stream;
+//   y     = ybuf[st->y_buf] + s_y r while st->y_applied < it — applied by the
+//          next k_price while it stages y in LDS;
+//   x_b  += s_x E with s_x = r.b while st->xb_applied < it — applied by the
+//          next k_update to the rows each wave owns.
+//   k_flush applies whatever is still pending (readback, end of a solve).
+//
+//   x_b, c_B, b (L), c (n), alpha[2], ybuf[2] (L), b_ixs (m int64).
 //   nb_list / nb_pos   this rank's non-basic columns (compact list + position,
 //          swap-remove / append per pivot) so pricing touches non-basic
 //          columns only.
@@ -42,12 +53,17 @@ struct alignas(16) DevState {
     int64_t iter;        // pivots made
     int64_t limit;       // kernels do nothing once iter >= limit
     int64_t p;           // last entering column
-    int64_t q;           // last leaving row
+    int64_t q;           // last pivot row (leaving position); -1 before any pivot
     double min_e;        // last entering reduced cost
     double z;            // objective (spx_objective)
+    double aq;           // alpha_q of the last pivot
+    double s_y;          // c_B_new.E_q + c_p - c_Bq of the last pivot (v4:354-355)
+    int64_t y_applied;   // ybuf[y_buf] includes the first y_applied pivots
+    int64_t xb_applied;  // x_b includes the first xb_applied pivots
+    int32_t y_buf;
     uint32_t ticket_price;
     uint32_t ticket_update;
-    int64_t pad[2];
+    int32_t pad0;
 };
 
 __host__ __device__ inline bool argmin_better(double v, int64_t j, double bv, int64_t bj) {
@@ -64,14 +80,13 @@ struct Params {
     // basis state
     double* B0;
     double* B1;
-    double* E0;
-    double* E1;
-    double* r0;
-    double* r1;
-    double* y;
+    double* alpha0;
+    double* alpha1;
+    double* y0;
+    double* y1;
     double* x_b;
     double* c_B;
-    double* alpha;
+    const double* zeros;   // L zeros (the "pivot row" before the first pivot)
     int64_t* b_ixs;
     int32_t* nb_list;
     int32_t* nb_pos;       // n entries, -1 when basic or not owned

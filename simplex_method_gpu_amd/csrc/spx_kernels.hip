@@ -1,23 +1,28 @@
 // spx_kernels.hip — gfx950 kernels of the dense revised-simplex hot loop.
 //
 // One loop pass is two launches (SURVEY.md §7 design notes):
-//   k_price   e_j = y.A_j - c_j over this rank's non-basic columns, fused with
-//             the entering argmin (v4:288-302).  One wave per column, A read
-//             with 16-byte loads, y staged once per workgroup in LDS, wave
-//             shuffle + LDS argmin, last-workgroup-done fan-in.
+//   k_price   stages y in LDS (applying the last pivot's y update on the fly),
+//             then e_j = y.A_j - c_j over this rank's non-basic columns fused
+//             with the entering argmin (v4:288-302).  One wave per column, A
+//             read with 16-byte non-temporal loads, wave shuffle + LDS argmin,
+//             last-workgroup-done fan-in.
 //   k_update  applies the pending rank-1 update B^-1 += E r^T (v4:331-333)
-//             while streaming B^-1 once, and in the same pass computes
-//             FTRAN alpha = B^-1_new A_p (v4:307-308); fused compute_theta +
-//             leaving argmin (v4:199-208,324); the last workgroup then forms
-//             E_q (v4:210-215), the pivot row r, and updates x_b, y, c_B and
-//             the basis (v4:339-357).
+//             while streaming B^-1 once, and in the same pass computes FTRAN
+//             alpha = B^-1_new A_p (v4:307-308), the last pivot's x_b update
+//             (v4:347-348) for the rows it owns, compute_theta and the leaving
+//             argmin (v4:199-208,324); the last workgroup then finds q, the
+//             y-update scalar (v4:352-355) and does the basis bookkeeping
+//             (v4:339-342).
 // Host synchronisation per pass: none.  Termination (optimum / unbounded /
 // iteration limit) is a device-side status word every kernel checks first.
+// The deferred pivot state is described in spx_device.h.
 //
 // Cross-workgroup hand-offs inside a launch (partials, alpha) use agent-scope
 // relaxed atomic stores/loads (global_* sc1: L1 bypass) drained with
 // s_waitcnt vmcnt(0) before a workgroup barrier and one agent-scope ticket
 // add per workgroup (MI355X_MICROARCH.md, Valid forms, first table row).
+// Everything is deterministic: fixed reduction orders, no float atomics, so
+// results are bit-identical for any grid / block size and any shard count.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <math.h>
@@ -28,6 +33,30 @@
 namespace spx {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+// Cache policy of the three big streams (compile-time; tools/policy_sweep.sh
+// builds the variants): 1 = non-temporal, 0 = default.  Measured at C3:
+// non-temporal loads of A cut k_price 93 -> 68 us, of B^-1 k_update 69 -> 56 us.
+#ifndef SPX_NT_A
+#define SPX_NT_A 1      // pricing reads of A
+#endif
+#ifndef SPX_NT_BLOAD
+#define SPX_NT_BLOAD 1  // update reads of B_old
+#endif
+#ifndef SPX_NT_BSTORE
+#define SPX_NT_BSTORE 1 // update writes of B_new
+#endif
+
+template <int NT>
+__device__ __forceinline__ dbl2 ld2(const dbl2* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -64,14 +93,59 @@ __device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned lo
         __hip_atomic_store(&slot[0], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-
-// Diagnostic sub-phase marks inside the update tail: slot 8+k accumulates the
-// ticks since the previous mark (thread 0 only).
+// Sub-phase marks inside the update tail: slot 8+k accumulates the ticks since
+// the previous mark (thread 0 only).
 __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, unsigned long long prev) {
     if (!P.stamps || threadIdx.x != 0) return prev;
     const unsigned long long now = rtime();
     atomicAdd(&P.stamps[8 + k], now - prev);
     return now;
+}
+
+// ---------------------------------------------------------------------------
+// Pieces of the deferred pivot (one definition, so every consumer — k_price,
+// k_update, k_flush, k_materialize — produces the same bits)
+// ---------------------------------------------------------------------------
+// compute_E_q (v4:210-215)
+__device__ __forceinline__ double eta_entry(double a_i, int64_t i, int64_t q, double aq) {
+    return (i != q) ? (-a_i / aq) : (1.0 / aq - 1.0);
+}
+// y += s_y r (v4:356)
+__device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
+    dbl2 o;
+    o.x = fma(s_y, r.x, y.x);
+    o.y = fma(s_y, r.y, y.y);
+    return o;
+}
+
+// s_x = r.b (v4:347) in a canonical order independent of the launch geometry:
+// NSLICE contiguous slices of the padded vectors, lane-strided pairs inside a
+// slice, slices summed in index order.  Each wave computes the slices
+// s = wave, wave + WAVES, ... into part[s]; call block_dot_finish after a
+// barrier.
+constexpr int NSLICE = 16;
+template <int WAVES>
+__device__ __forceinline__ void block_dot_slices(const double* r, const double* b, int64_t L, double* part) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t len = (L >> 1) / NSLICE;  // L is a multiple of 128
+    for (int s = wave; s < NSLICE; s += WAVES) {
+        const dbl2* r2 = reinterpret_cast<const dbl2*>(r) + s * len;
+        const dbl2* b2 = reinterpret_cast<const dbl2*>(b) + s * len;
+        double a0 = 0.0, a1 = 0.0;
+        for (int64_t k = lane; k < len; k += 64) {
+            const dbl2 x = r2[k], z = b2[k];
+            a0 = fma(x.x, z.x, a0);
+            a1 = fma(x.y, z.y, a1);
+        }
+        const double v = wave_sum(a0 + a1);
+        if (lane == 0) part[s] = v;
+    }
+}
+__device__ __forceinline__ double block_dot_finish(const double* part) {
+    double s = part[0];
+#pragma unroll
+    for (int k = 1; k < NSLICE; ++k) s += part[k];
+    return s;
 }
 
 // ---------------------------------------------------------------------------
@@ -95,13 +169,29 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
+    // current y = ybuf + s_y r when the last pivot's y update is pending
+    const int64_t it = st->iter;
+    const bool upd_y = st->y_applied < it;
+    const double s_y = st->s_y;
+    const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
+    dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
+    const dbl2* rr = reinterpret_cast<const dbl2*>(upd_y ? ((it & 1) ? P.B1 : P.B0) + st->q * L : P.zeros);
     if constexpr (LDS_Y) {
-        const dbl2* yg = reinterpret_cast<const dbl2*>(P.y);
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
-        for (int64_t k = tid; k < L2; k += BLOCK) yl[k] = yg[k];
+        for (int64_t k = tid; k < L2; k += BLOCK) {
+            const dbl2 v = upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
+            yl[k] = v;
+            if (upd_y && blockIdx.x == 0) yout[k] = v;  // persisted once (flipped by k_update's tail)
+        }
         __syncthreads();
+    } else {
+        if (upd_y && blockIdx.x == 0)
+            for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(s_y, rr[k], yin[k]);
     }
-    const dbl2* y2 = LDS_Y ? reinterpret_cast<const dbl2*>(ys) : reinterpret_cast<const dbl2*>(P.y);
+    auto Y = [&](int64_t k) -> dbl2 {
+        if constexpr (LDS_Y) return reinterpret_cast<const dbl2*>(ys)[k];
+        else return upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
+    };
 
     const int nb = st->nb_count;
     double best = INFINITY;
@@ -114,17 +204,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         for (; k + 7 * 64 < L2; k += 8 * 64) {
             dbl2 v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(&col[k + u * 64]);
+            for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const dbl2 w = y2[k + u * 64];
+                const dbl2 w = Y(k + u * 64);
                 a0 = fma(v[u].x, w.x, a0);
                 a1 = fma(v[u].y, w.y, a1);
             }
         }
         for (; k < L2; k += 64) {
-            const dbl2 v = __builtin_nontemporal_load(&col[k]);
-            const dbl2 w = y2[k];
+            const dbl2 v = ld2<SPX_NT_A>(&col[k]);
+            const dbl2 w = Y(k);
             a0 = fma(v.x, w.x, a0);
             a1 = fma(v.y, w.y, a1);
         }
@@ -157,45 +247,42 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         const int64_t i = ld_agent(&P.price_partials[g].idx);
         if (argmin_better(v, i, w.val, w.idx)) w = ArgMinEntry{v, i};
     }
-    red[tid] = w;
-    __syncthreads();
-    for (int s = BLOCK / 2; s > 0; s >>= 1) {
-        if (tid < s && argmin_better(red[tid + s].val, red[tid + s].idx, red[tid].val, red[tid].idx))
-            red[tid] = red[tid + s];
-        __syncthreads();
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double v = __shfl_xor(w.val, off, 64);
+        const int64_t i = __shfl_xor(w.idx, off, 64);
+        if (argmin_better(v, i, w.val, w.idx)) w = ArgMinEntry{v, i};
     }
+    __syncthreads();
+    if (lane == 0) red[wave] = w;
+    __syncthreads();
     if (tid == 0) {
-        *P.price_out = red[0];
+        ArgMinEntry t = red[0];
+        for (int i = 1; i < WAVES; ++i)
+            if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
+        *P.price_out = t;
         st_agent(&st->ticket_price, 0u);
     }
     stamp_tail(slot, t_tail);
 }
 
 // ---------------------------------------------------------------------------
-// Fused: pending rank-1 update + FTRAN + ratio test + leaving argmin + tail
+// Fused: pending rank-1 update + FTRAN + x_b update + ratio test + leaving
+// argmin + pivot tail
 // ---------------------------------------------------------------------------
-// Block-wide sum of two doubles: wave butterflies, then one LDS pass over the
-// per-wave sums in wave order (deterministic for a fixed BLOCK).
+// Block-wide sum: wave butterflies, then the per-wave sums in wave order.
 template <int BLOCK>
-__device__ void block_sum2(double& a, double& b, double* sa, double* sb) {
+__device__ double block_sum(double a, double* sa) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) {
-        sa[wave] = a;
-        sb[wave] = b;
-    }
+    if (lane == 0) sa[wave] = a;
     __syncthreads();
-    double ta = sa[0], tb = sb[0];
+    double t = sa[0];
 #pragma unroll
-    for (int w = 1; w < WAVES; ++w) {
-        ta += sa[w];
-        tb += sb[w];
-    }
-    a = ta;
-    b = tb;
+    for (int w = 1; w < WAVES; ++w) t += sa[w];
     __syncthreads();
+    return t;
 }
 
 // Leaving argmin over the k_update workgroup partials + unbounded count
@@ -232,75 +319,53 @@ __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red) {
 }
 
 struct TailShared {
-    double aq, eq, c_bq;
+    double aq, c_bq;
     int64_t leave;
+    int64_t pad;
 };
 
-// Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and the
-// loop counters; thread 0 only, after every other use of c_B / b_ixs.
-__device__ __forceinline__ void tail_bookkeeping(const Params& P, DevState* st, int64_t p, int64_t q, double c_p,
-                                                 int64_t leave, int cnt, int kp, int last, bool own_p,
-                                                 double min_e, int64_t it) {
-    P.c_B[q] = c_p;
-    P.b_ixs[q] = p;
-    if (own_p) {
-        P.nb_list[kp] = last;
-        P.nb_pos[last] = kp;
-        P.nb_pos[p] = -1;
-        --cnt;
-    }
-    if (owns_col(P, leave)) {
-        P.nb_list[cnt] = (int32_t)leave;
-        P.nb_pos[leave] = cnt;
-        ++cnt;
-    }
-    st->nb_count = cnt;
-    st->p = p;
-    st->q = q;
-    st->min_e = min_e;
-    st->iter = it + 1;
-    st_agent(&st->ticket_update, 0u);
-}
+// LDS carve-up of k_update (dynamic, 16-byte aligned pieces)
+template <int BLOCK>
+struct UpdLds {
+    static constexpr int WAVES = BLOCK / 64;
+    static constexpr size_t red = 0;                                        // UpdPartial[WAVES]
+    static constexpr size_t shared = red + sizeof(UpdPartial) * WAVES;      // TailShared
+    static constexpr size_t sums = shared + sizeof(TailShared);             // double[WAVES]
+    static constexpr size_t slices = sums + 8 * ((WAVES + 1) / 2 * 2);      // double[NSLICE]
+    static constexpr size_t last = slices + 8 * NSLICE;                     // int
+    static constexpr size_t bytes = last + 16;
+};
 
-__device__ __forceinline__ void tail_unbounded(DevState* st, int64_t p, double min_e) {
-    st->p = p;
-    st->min_e = min_e;
-    st->q = -1;
-    st->status = ST_UNBOUNDED;
-    st_agent(&st->ticket_update, 0u);
-}
-
-// Runs in the last workgroup of k_update: everything after the leaving argmin
-// (v4:317-357) on O(m) vectors.  Latency-bound (one workgroup, the rest of the
-// GPU idle), so it is built around two dependent memory round trips: the
-// inputs that do not depend on q (alpha, c_B, b, r_prev and the list words of
-// p) are loaded before the partial reduction that yields q; B_old[q,:], x_b, y
-// and row q's scalars are loaded together right after it.
-// Needs m <= CH * BLOCK (one element chunk per thread held in registers).
-template <int BLOCK, int CH>
-__device__ void update_tail_regs(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
-                                 unsigned char* smem) {
-    constexpr int WAVES = BLOCK / 64;
+// The last workgroup of k_update: leaving row q, unboundedness (v4:317-325),
+// alpha_q, s_y = c_B_new.E_q + c_p - c_Bq (v4:352-355) and the basis
+// bookkeeping (v4:339-342).  The vector updates themselves are deferred (see
+// spx_device.h), so this is one dependent round trip: the alpha / c_B / b_ixs
+// loads are issued together with the partial loads, row q's scalars are
+// broadcast through LDS from the thread that loaded them.
+template <int BLOCK>
+__device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
+                            bool y_was_pending, const double* a_new, unsigned char* smem) {
+    using Lds = UpdLds<BLOCK>;
+    constexpr int CH = 4;
     const int tid = threadIdx.x;
-    const int64_t m = P.m, L = P.L;
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
+    const int64_t m = P.m;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
+    TailShared* sh = reinterpret_cast<TailShared*>(smem + Lds::shared);
+    double* sums = reinterpret_cast<double*>(smem + Lds::sums);
+    const bool in_regs = m <= (int64_t)CH * BLOCK;
 
-    const double* Bsrc = par ? P.B1 : P.B0;
-    const double* Ep = par ? P.E1 : P.E0;
-    const double* rp = par ? P.r1 : P.r0;
-    double* Ec = par ? P.E0 : P.E1;
-    double* rc = par ? P.r0 : P.r1;
-
-    // round trip 1 (overlaps the partial loads): everything independent of q
-    double a[CH], cb[CH], bb[CH], rr[CH];
+    unsigned long long tm = P.stamps ? rtime() : 0;
+    double a[CH], cb[CH];
+    int64_t bx[CH];
+    if (in_regs) {
 #pragma unroll
-    for (int u = 0; u < CH; ++u) {
-        const int64_t i = (int64_t)u * BLOCK + tid;
-        if (i < m) {
-            a[u] = ld_agent(&P.alpha[i]);
-            cb[u] = P.c_B[i];
-            bb[u] = P.b[i];
-            rr[u] = rp[i];
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = (int64_t)u * BLOCK + tid;
+            if (i < m) {
+                a[u] = ld_agent(&a_new[i]);
+                cb[u] = P.c_B[i];
+                bx[u] = P.b_ixs[i];
+            }
         }
     }
     const double c_p = P.c[p];
@@ -314,170 +379,87 @@ __device__ void update_tail_regs(const Params& P, DevState* st, int64_t p, doubl
         }
     }
 
-    unsigned long long tm = P.stamps ? rtime() : 0;
     const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
     tm = tail_mark(P, 0, tm);
     const int64_t q = t.idx;
-    if (t.nonpos == m || q < 0 || q >= m) {  // Unbounded (v4:319-322)
-        if (tid == 0) tail_unbounded(st, p, min_e);
+    if (t.nonpos == m || q < 0 || q >= m) {
+        // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no
+        // valid candidate (NaN-poisoned x_b) stops the same way.  The deferred
+        // state of the previous pivot (q, aq, s_y) is left intact for k_flush.
+        if (tid == 0) {
+            st->p = p;
+            st->min_e = min_e;
+            st->status = ST_UNBOUNDED;
+            st_agent(&st->ticket_update, 0u);
+        }
         return;
     }
-
-    // round trip 2: row q of B_old, x_b, y and row q's scalars
-    const double* brow = Bsrc + q * L;
-    double br[CH], xv[CH], yv[CH];
+    double aq, c_bq;
+    int64_t leave;
+    if (in_regs) {
 #pragma unroll
-    for (int u = 0; u < CH; ++u) {
-        const int64_t i = (int64_t)u * BLOCK + tid;
-        if (i < m) {
-            br[u] = brow[i];
-            xv[u] = P.x_b[i];
-            yv[u] = P.y[i];
+        for (int u = 0; u < CH; ++u) {
+            if ((int64_t)u * BLOCK + tid == q) {
+                sh->aq = a[u];
+                sh->c_bq = cb[u];
+                sh->leave = bx[u];
+            }
         }
+        __syncthreads();
+        aq = sh->aq;
+        c_bq = sh->c_bq;
+        leave = sh->leave;
+    } else {
+        aq = ld_agent(&a_new[q]);
+        c_bq = P.c_B[q];
+        leave = P.b_ixs[q];
     }
-    const double aq = ld_agent(&P.alpha[q]);
-    const double eq = Ep[q];
-    const double c_bq = P.c_B[q];
-    int64_t leave = 0;
-    if (tid == 0) leave = P.b_ixs[q];
 
-    // E_q (compute_E_q, v4:210-215); r = B^-1_new[q,:] (v4:331) exactly as the
-    // streaming pass wrote it; s_x = r.b (v4:347); s_y = c_B_new.E_q (v4:354)
-    double sx = 0.0, sy = 0.0;
+    // s_y = c_B_new . E_q (v4:354) with c_B_new[q] = c_p (v4:340)
+    double sy = 0.0;
+    if (in_regs) {
 #pragma unroll
-    for (int u = 0; u < CH; ++u) {
-        const int64_t i = (int64_t)u * BLOCK + tid;
-        if (i < m) {
-            a[u] = (i != q) ? (-a[u] / aq) : (1.0 / aq - 1.0);  // a[] now holds E_q
-            rr[u] = fma(eq, rr[u], br[u]);                       // rr[] now holds r
-            sx = fma(rr[u], bb[u], sx);
-            sy = fma((i == q) ? c_p : cb[u], a[u], sy);
+        for (int u = 0; u < CH; ++u) {
+            const int64_t i = (int64_t)u * BLOCK + tid;
+            if (i < m) sy = fma((i == q) ? c_p : cb[u], eta_entry(a[u], i, q, aq), sy);
         }
+    } else {
+        for (int64_t i = tid; i < m; i += BLOCK)
+            sy = fma((i == q) ? c_p : P.c_B[i], eta_entry(ld_agent(&a_new[i]), i, q, aq), sy);
     }
     tm = tail_mark(P, 1, tm);
-    double* sa = reinterpret_cast<double*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared));
-    double* sb = sa + WAVES;
-    block_sum2<BLOCK>(sx, sy, sa, sb);
+    sy = block_sum<BLOCK>(sy, sums);
     tm = tail_mark(P, 2, tm);
-    const double s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
-    // x_b += s_x E_q (v4:348); y += s_y r (v4:356)
-#pragma unroll
-    for (int u = 0; u < CH; ++u) {
-        const int64_t i = (int64_t)u * BLOCK + tid;
-        if (i < m) {
-            Ec[i] = a[u];
-            rc[i] = rr[u];
-            P.x_b[i] = fma(sx, a[u], xv[u]);
-            P.y[i] = fma(s_y, rr[u], yv[u]);
-        }
-    }
-    __syncthreads();
-    tm = tail_mark(P, 3, tm);
-    if (tid == 0) tail_bookkeeping(P, st, p, q, c_p, leave, cnt, kp, last, own_p, min_e, it);
-    tm = tail_mark(P, 4, tm);
-}
 
-// General tail for m > CH * BLOCK: the same steps in element chunks.
-template <int BLOCK>
-__device__ void update_tail_loop(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
-                                 unsigned char* smem) {
-    constexpr int WAVES = BLOCK / 64;
-    constexpr int CH = 4;
-    const int tid = threadIdx.x;
-    const int64_t m = P.m, L = P.L;
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
-
-    const double c_p = P.c[p];
-    const bool own_p = owns_col(P, p);
-    int cnt = 0, kp = -1, last = -1;
     if (tid == 0) {
-        cnt = st->nb_count;
+        // basis bookkeeping (v4:339-342) + non-basic list swap-remove / append
+        P.c_B[q] = c_p;
+        P.b_ixs[q] = p;
         if (own_p) {
-            kp = P.nb_pos[p];
-            last = P.nb_list[cnt - 1];
+            P.nb_list[kp] = last;
+            P.nb_pos[last] = kp;
+            P.nb_pos[p] = -1;
+            --cnt;
         }
+        if (owns_col(P, leave)) {
+            P.nb_list[cnt] = (int32_t)leave;
+            P.nb_pos[leave] = cnt;
+            ++cnt;
+        }
+        st->nb_count = cnt;
+        // the deferred pivot (spx_device.h)
+        st->aq = aq;
+        st->s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+        if (y_was_pending) st->y_buf ^= 1;  // k_price of this pass persisted y
+        st->y_applied = it;
+        st->xb_applied = it;
+        st->p = p;
+        st->q = q;
+        st->min_e = min_e;
+        st->iter = it + 1;
+        st_agent(&st->ticket_update, 0u);
     }
-    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
-    const int64_t q = t.idx;
-    if (t.nonpos == m || q < 0 || q >= m) {
-        if (tid == 0) tail_unbounded(st, p, min_e);
-        return;
-    }
-    const double* Bsrc = par ? P.B1 : P.B0;
-    const double* Ep = par ? P.E1 : P.E0;
-    const double* rp = par ? P.r1 : P.r0;
-    double* Ec = par ? P.E0 : P.E1;
-    double* rc = par ? P.r0 : P.r1;
-    const double* brow = Bsrc + q * L;
-    const double aq = ld_agent(&P.alpha[q]);
-    const double eq = Ep[q];
-    const double c_bq = P.c_B[q];
-    const int64_t leave = P.b_ixs[q];
-
-    double sx = 0.0, sy = 0.0;
-    for (int64_t base = 0; base < m; base += (int64_t)CH * BLOCK) {
-        double a[CH], cb[CH], bb[CH], br[CH], rr[CH];
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = base + (int64_t)u * BLOCK + tid;
-            if (i < m) {
-                a[u] = ld_agent(&P.alpha[i]);
-                cb[u] = P.c_B[i];
-                bb[u] = P.b[i];
-                br[u] = brow[i];
-                rr[u] = rp[i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = base + (int64_t)u * BLOCK + tid;
-            if (i < m) {
-                const double e = (i != q) ? (-a[u] / aq) : (1.0 / aq - 1.0);
-                const double r = fma(eq, rr[u], br[u]);
-                Ec[i] = e;
-                rc[i] = r;
-                sx = fma(r, bb[u], sx);
-                sy = fma((i == q) ? c_p : cb[u], e, sy);
-            }
-        }
-    }
-    double* sa = reinterpret_cast<double*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared));
-    double* sb = sa + WAVES;
-    block_sum2<BLOCK>(sx, sy, sa, sb);
-    const double s_y = sy + (c_p - c_bq);
-    for (int64_t base = 0; base < m; base += (int64_t)CH * BLOCK) {
-        double xv[CH], yv[CH], ev[CH], rv[CH];
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = base + (int64_t)u * BLOCK + tid;
-            if (i < m) {
-                xv[u] = P.x_b[i];
-                yv[u] = P.y[i];
-                ev[u] = Ec[i];
-                rv[u] = rc[i];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = base + (int64_t)u * BLOCK + tid;
-            if (i < m) {
-                P.x_b[i] = fma(sx, ev[u], xv[u]);
-                P.y[i] = fma(s_y, rv[u], yv[u]);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) tail_bookkeeping(P, st, p, q, c_p, leave, cnt, kp, last, own_p, min_e, it);
-}
-
-template <int BLOCK>
-__device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it, int par,
-                            unsigned char* smem) {
-    constexpr int CH = 4;
-    if (P.m <= (int64_t)CH * BLOCK)
-        update_tail_regs<BLOCK, CH>(P, st, p, min_e, it, par, smem);
-    else
-        update_tail_loop<BLOCK>(P, st, p, min_e, it, par, smem);
+    tm = tail_mark(P, 3, tm);
 }
 
 template <int BLOCK, int R>
@@ -486,6 +468,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if (stopped(st)) return;
     unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
     stamp_start(slot);
+    using Lds = UpdLds<BLOCK>;
     constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
@@ -511,18 +494,31 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t it = st->iter;
     const int par = (int)(it & 1);
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
-    const dbl2* __restrict__ src = reinterpret_cast<const dbl2*>(par ? P.B1 : P.B0);
+    const double* S = par ? P.B1 : P.B0;
+    const dbl2* __restrict__ src = reinterpret_cast<const dbl2*>(S);
     dbl2* __restrict__ dst = reinterpret_cast<dbl2*>(par ? P.B0 : P.B1);
-    const double* Ep = par ? P.E1 : P.E0;
-    const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(par ? P.r1 : P.r0);
+    const double* a_prev = par ? P.alpha1 : P.alpha0;  // alpha of pivot it-1
+    double* a_new = par ? P.alpha0 : P.alpha1;
+    // the pending pivot it-1: r = S[q,:], E from a_prev and aq
+    const bool pend = it > 0;
+    const int64_t qp = st->q;
+    const double aqp = st->aq;
+    const double* rrow = pend ? S + qp * L : P.zeros;
+    const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(rrow);
     const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
+    const bool upd_x = st->xb_applied < it;
+    const bool y_was_pending = st->y_applied < it;
+
+    // s_x = r.b for the deferred x_b update: slice partials now, sum after the stream
+    double* slices = reinterpret_cast<double*>(smem + Lds::slices);
+    if (upd_x) block_dot_slices<WAVES>(rrow, P.b, L, slices);
 
     const int64_t row0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
     const int nvalid = (int)((row0 >= m) ? 0 : ((m - row0 < R) ? (m - row0) : R));
     double ei[R], acc[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-        ei[u] = (u < nvalid) ? Ep[row0 + u] : 0.0;
+        ei[u] = (pend && u < nvalid) ? eta_entry(a_prev[row0 + u], row0 + u, qp, aqp) : 0.0;
         acc[u] = 0.0;
     }
     const int64_t base = row0 * L2;
@@ -536,7 +532,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 rv[t] = rp[k + t * 64];
                 av[t] = ap[k + t * 64];
 #pragma unroll
-                for (int u = 0; u < R; ++u) bv[t][u] = __builtin_nontemporal_load(&src[base + u * L2 + k + t * 64]);
+                for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
             }
 #pragma unroll
             for (int t = 0; t < U; ++t) {
@@ -545,7 +541,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                     dbl2 nv;
                     nv.x = fma(ei[u], rv[t].x, bv[t][u].x);
                     nv.y = fma(ei[u], rv[t].y, bv[t][u].y);
-                    __builtin_nontemporal_store(nv, &dst[base + u * L2 + k + t * 64]);
+                    st2<SPX_NT_BSTORE>(nv, &dst[base + u * L2 + k + t * 64]);
                     acc[u] = fma(nv.x, av[t].x, acc[u]);
                     acc[u] = fma(nv.y, av[t].y, acc[u]);
                 }
@@ -579,7 +575,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
     }
 
-    // alpha_i, theta_i (compute_theta, v4:199-208) and the wave's argmin
+    __syncthreads();  // slice partials of s_x
+    const double s_x = upd_x ? block_dot_finish(slices) : 0.0;
+
+    // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
+    // (compute_theta, v4:199-208) and the wave's argmin
     double wbest = INFINITY;
     int64_t wi = INT64_MAX;
     int64_t nonpos = 0;
@@ -588,16 +588,21 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         if (u < nvalid) {
             const double a = wave_sum(acc[u]);
             const int64_t i = row0 + u;
-            if (lane == 0) st_agent(&P.alpha[i], a);
+            double xb = P.x_b[i];
+            if (upd_x) xb = fma(s_x, ei[u], xb);
+            if (lane == 0) {
+                st_agent(&a_new[i], a);
+                if (upd_x) P.x_b[i] = xb;
+            }
             const bool pos = a > 0.0;
-            const double th = pos ? P.x_b[i] / a : INFINITY;
+            const double th = pos ? xb / a : INFINITY;
             nonpos += !pos;
             if (argmin_better(th, i, wbest, wi)) { wbest = th; wi = i; }
         }
     }
     drain_vmem();  // every storing wave drains its alpha stores before the barrier
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem);
-    int* s_last = reinterpret_cast<int*>(smem + sizeof(UpdPartial) * WAVES + sizeof(TailShared) + 16 * WAVES);
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
+    int* s_last = reinterpret_cast<int*>(smem + Lds::last);
     if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, 0};
     __syncthreads();
     if (tid == 0) {
@@ -617,12 +622,95 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     __syncthreads();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
-    update_tail<BLOCK>(P, st, p, min_e, it, par, smem);
+    update_tail<BLOCK>(P, st, p, min_e, it, y_was_pending, a_new, smem);
     stamp_tail(slot, t_tail);
 }
 
 // ---------------------------------------------------------------------------
-// Setup / readback kernels (off the hot loop)
+// Deferred-state flush and readback kernels (off the hot loop)
+// ---------------------------------------------------------------------------
+// Applies the pending y and x_b updates of the last pivot (one workgroup).
+__global__ __launch_bounds__(1024) void k_flush(Params P) {
+    constexpr int BLOCK = 1024, WAVES = BLOCK / 64;
+    __shared__ double slices[NSLICE];
+    DevState* st = P.st;
+    const int tid = threadIdx.x;
+    const int64_t it = st->iter, L = P.L, L2 = L >> 1, m = P.m;
+    if (it == 0) return;
+    const double* S = (it & 1) ? P.B1 : P.B0;
+    const double* r = S + st->q * L;
+    const bool upd_y = st->y_applied < it, upd_x = st->xb_applied < it;
+    if (upd_y) {
+        const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
+        dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
+        const dbl2* r2 = reinterpret_cast<const dbl2*>(r);
+        for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(st->s_y, r2[k], yin[k]);
+    }
+    if (upd_x) {
+        block_dot_slices<WAVES>(r, P.b, L, slices);
+        __syncthreads();
+        const double s_x = block_dot_finish(slices);
+        const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
+        const int64_t q = st->q;
+        const double aq = st->aq;
+        for (int64_t i = tid; i < m; i += BLOCK) P.x_b[i] = fma(s_x, eta_entry(a_prev[i], i, q, aq), P.x_b[i]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        if (upd_y) {
+            st->y_buf ^= 1;
+            st->y_applied = it;
+        }
+        if (upd_x) st->xb_applied = it;
+    }
+}
+
+// true B^-1 = S + E r^T into out (m x L row-major)
+__global__ void k_materialize(Params P, double* out) {
+    const DevState* st = P.st;
+    const int64_t it = st->iter;
+    const double* S = (it & 1) ? P.B1 : P.B0;
+    const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
+    const int64_t q = st->q;
+    const double aq = st->aq;
+    const int64_t total = P.m * P.L;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / P.L, k = t - i * P.L;
+        out[t] = (it > 0) ? fma(eta_entry(a_prev[i], i, q, aq), S[q * P.L + k], S[t]) : S[t];
+    }
+}
+
+// e_j for every column from the current (flushed) y, one wave per column
+__global__ __launch_bounds__(256) void k_reduced_costs(Params P, double* e) {
+    const int lane = threadIdx.x & 63;
+    const int64_t L2 = P.L >> 1;
+    const dbl2* y2 = reinterpret_cast<const dbl2*>(P.st->y_buf ? P.y1 : P.y0);
+    for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < P.n;
+         j += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const dbl2* col = reinterpret_cast<const dbl2*>(P.A + j * P.L);
+        double a0 = 0.0, a1 = 0.0;
+        for (int64_t k = lane; k < L2; k += 64) {
+            const dbl2 v = col[k], w = y2[k];
+            a0 = fma(v.x, w.x, a0);
+            a1 = fma(v.y, w.y, a1);
+        }
+        const double s = wave_sum(a0 + a1) - P.c[j];
+        if (lane == 0) e[j] = s;
+    }
+}
+
+// z = c_B . x_b (v4:365), from the flushed x_b
+__global__ __launch_bounds__(256) void k_objective(Params P) {
+    __shared__ double sa[4];
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < P.m; i += 256) s = fma(P.c_B[i], P.x_b[i], s);
+    s = block_sum<256>(s, sa);
+    if (threadIdx.x == 0) P.st->z = s;
+}
+
+// ---------------------------------------------------------------------------
+// Setup kernels
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ULL;
@@ -650,16 +738,16 @@ __global__ void k_generate(double* A, double* b, double* c, int64_t m, int64_t n
     }
 }
 
-// slack basis (v4:268-277 with the intended semantics)
+// slack basis (v4:268-277 with the intended semantics); vectors zeroed by the host
 __global__ void k_reset(Params P) {
     const int64_t m = P.m, n = P.n, L = P.L, ns = P.ns;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = t0; i < m; i += stride) {
-        P.B0[i * L + i] = 1.0;  // init_I (v4:182-188); buffers zeroed by the host
+        P.B0[i * L + i] = 1.0;  // init_I (v4:182-188)
         P.c_B[i] = P.c[ns + i];
         P.x_b[i] = P.b[i];
-        P.y[i] = P.c[ns + i];
+        P.y0[i] = P.c[ns + i];
         P.b_ixs[i] = ns + i;
     }
     for (int64_t j = t0; j < n; j += stride) {
@@ -680,64 +768,24 @@ __global__ void k_reset(Params P) {
         st->q = -1;
         st->min_e = 0.0;
         st->z = 0.0;
+        st->aq = 1.0;
+        st->s_y = 0.0;
+        st->y_applied = 0;
+        st->xb_applied = 0;
+        st->y_buf = 0;
         st->ticket_price = 0;
         st->ticket_update = 0;
     }
-    (void)L;
-}
-
-// B^-1 with the pending update applied, into out (m x L row-major)
-__global__ void k_materialize(Params P, double* out) {
-    const DevState* st = P.st;
-    const int par = (int)(st->iter & 1);
-    const double* B = par ? P.B1 : P.B0;
-    const double* E = par ? P.E1 : P.E0;
-    const double* r = par ? P.r1 : P.r0;
-    const int64_t total = P.m * P.L;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = t / P.L, k = t - i * P.L;
-        out[t] = fma(E[i], r[k], B[t]);
-    }
-}
-
-// e_j for every column (debug / parity), one wave per column
-__global__ __launch_bounds__(256) void k_reduced_costs(Params P, double* e) {
-    const int lane = threadIdx.x & 63;
-    const int64_t L2 = P.L >> 1;
-    const dbl2* y2 = reinterpret_cast<const dbl2*>(P.y);
-    for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < P.n;
-         j += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const dbl2* col = reinterpret_cast<const dbl2*>(P.A + j * P.L);
-        double a0 = 0.0, a1 = 0.0;
-        for (int64_t k = lane; k < L2; k += 64) {
-            const dbl2 v = col[k], w = y2[k];
-            a0 = fma(v.x, w.x, a0);
-            a1 = fma(v.y, w.y, a1);
-        }
-        const double s = wave_sum(a0 + a1) - P.c[j];
-        if (lane == 0) e[j] = s;
-    }
-}
-
-// z = c_B . x_b (v4:365)
-__global__ __launch_bounds__(256) void k_objective(Params P) {
-    __shared__ double sa[256], sb[256];
-    double s = 0.0, d = 0.0;
-    for (int64_t i = threadIdx.x; i < P.m; i += 256) s = fma(P.c_B[i], P.x_b[i], s);
-    block_sum2<256>(s, d, sa, sb);
-    if (threadIdx.x == 0) P.st->z = s;
 }
 
 // ---------------------------------------------------------------------------
 // Host-side launchers
 // ---------------------------------------------------------------------------
 template <int BLOCK, bool LDS_Y>
-static hipError_t launch_price_t(const Params& P, int grid, size_t lds, hipStream_t s,
-                                 hipEvent_t e0, hipEvent_t e1) {
+static hipError_t launch_price_t(const Params& P, int grid, size_t lds, hipStream_t s, hipEvent_t e0,
+                                 hipEvent_t e1) {
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1,
-                              0, P);
+        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
         hipLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
@@ -791,7 +839,7 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
 
 template <int BLOCK, int R>
 static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const size_t lds = sizeof(UpdPartial) * (BLOCK / 64) + sizeof(TailShared) + 16 * (BLOCK / 64) + 16;
+    const size_t lds = UpdLds<BLOCK>::bytes;
     if (e0 || e1) {
         hipExtLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
@@ -838,6 +886,11 @@ hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n
 hipError_t launch_reset(const Params& P, hipStream_t s) {
     const int64_t w = P.m > P.n ? P.m : P.n;
     hipLaunchKernelGGL(k_reset, dim3(grid_for(w, 256)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_flush(const Params& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_flush, dim3(1), dim3(1024), 0, s, P);
     return hipGetLastError();
 }
 
