@@ -77,6 +77,8 @@ typedef struct spx_opts {
 
 #define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times)  */
 #define SPX_FLAG_STAMPS 2 /* in-kernel phase stamps (spx_phase_times); diagnostic */
+#define SPX_FLAG_GLOBAL_Y 4 /* pricing reads y from global memory instead of LDS
+                               (automatic when L*8 bytes do not fit in LDS)   */
 
 void spx_default_opts(spx_opts* opts);
 

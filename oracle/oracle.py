@@ -100,6 +100,16 @@ def generate_np(m: int, n: int, seed: int):
     return A, b, c
 
 
+def column_np(m: int, n: int, seed: int, j: int) -> np.ndarray:
+    """Column j of the generated A (for spot checks at sizes too big to build)."""
+    if j >= n - m:
+        e = np.zeros(m)
+        e[j - (n - m)] = 1.0
+        return e
+    idx = np.arange(m, dtype=np.uint64) + np.uint64(j) * np.uint64(m)
+    return uniform_np(seed, 1, idx)
+
+
 def generate(m: int, n: int, seed: int):
     """C generator; returns (A_cols (n, m) C-contiguous == column-major m x n, b, c)."""
     A = np.empty((n, m), dtype=np.float64)

@@ -28,6 +28,7 @@ __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_un
 
 FLAG_TIMING = 1
 FLAG_STAMPS = 2
+FLAG_GLOBAL_Y = 4
 
 
 class SolveStatus(IntEnum):
@@ -108,14 +109,16 @@ class Context:
     def __init__(self, A_cols=None, b=None, c=None, *, m: int | None = None, n: int | None = None,
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
-                 update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False):
+                 update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
+                 global_y: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
         o.eps, o.device, o.rank, o.nranks = eps, device, rank, nranks
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
         o.update_block = update_block
-        o.flags = (FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
+        o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
+                   | (FLAG_GLOBAL_Y if global_y else 0))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)

@@ -234,7 +234,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         pc.block = x->opts.price_block;
     else
         pc.block = ybytes <= 72 * 1024 ? 512 : 1024;
-    pc.lds_y = ybytes + (size_t)pc.block * 16 + 16 <= 150 * 1024;
+    pc.lds_y = ybytes + (size_t)pc.block * 16 + 16 <= 150 * 1024 && !(x->opts.flags & SPX_FLAG_GLOBAL_Y);
     pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (size_t)pc.block * sizeof(ArgMinEntry) + 16;
     int per_cu = 0;
     HIP_TRY(price_prepare(pc, &per_cu));

@@ -339,32 +339,36 @@ struct UpdLds {
 // The last workgroup of k_update: leaving row q, unboundedness (v4:317-325),
 // alpha_q, s_y = c_B_new.E_q + c_p - c_Bq (v4:352-355) and the basis
 // bookkeeping (v4:339-342).  The vector updates themselves are deferred (see
-// spx_device.h), so this is one dependent round trip: the alpha / c_B / b_ixs
-// loads are issued together with the partial loads, row q's scalars are
-// broadcast through LDS from the thread that loaded them.
+// spx_device.h), so this is one dependent round trip: with 16 waves and
+// L <= 4096 the alpha / c_B / b_ixs loads are issued together with the
+// partial loads and row q's scalars are broadcast through LDS from the lane
+// that loaded them; otherwise they are loaded after q.  s_y's dot product
+// uses the canonical slice order of block_dot_slices (geometry-independent).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
                             bool y_was_pending, const double* a_new, unsigned char* smem) {
     using Lds = UpdLds<BLOCK>;
+    constexpr int WAVES = BLOCK / 64;
     constexpr int CH = 4;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t m = P.m;
+    const int64_t len = P.L / NSLICE;  // elements per slice
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     TailShared* sh = reinterpret_cast<TailShared*>(smem + Lds::shared);
-    double* sums = reinterpret_cast<double*>(smem + Lds::sums);
-    const bool in_regs = m <= (int64_t)CH * BLOCK;
+    double* part = reinterpret_cast<double*>(smem + Lds::slices);
+    const bool in_regs = (WAVES == NSLICE) && (len <= 64 * CH);
 
     unsigned long long tm = P.stamps ? rtime() : 0;
     double a[CH], cb[CH];
     int64_t bx[CH];
     if (in_regs) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = (int64_t)u * BLOCK + tid;
-            if (i < m) {
-                a[u] = ld_agent(&a_new[i]);
-                cb[u] = P.c_B[i];
-                bx[u] = P.b_ixs[i];
+        for (int t = 0; t < CH; ++t) {
+            const int64_t k = lane + 64 * t, i = wave * len + k;
+            if (k < len && i < m) {
+                a[t] = ld_agent(&a_new[i]);
+                cb[t] = P.c_B[i];
+                bx[t] = P.b_ixs[i];
             }
         }
     }
@@ -379,10 +383,10 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
         }
     }
 
-    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
+    const UpdPartial t0 = reduce_update_partials<BLOCK>(P, red);
     tm = tail_mark(P, 0, tm);
-    const int64_t q = t.idx;
-    if (t.nonpos == m || q < 0 || q >= m) {
+    const int64_t q = t0.idx;
+    if (t0.nonpos == m || q < 0 || q >= m) {
         // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no
         // valid candidate (NaN-poisoned x_b) stops the same way.  The deferred
         // state of the previous pivot (q, aq, s_y) is left intact for k_flush.
@@ -398,11 +402,11 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
     int64_t leave;
     if (in_regs) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            if ((int64_t)u * BLOCK + tid == q) {
-                sh->aq = a[u];
-                sh->c_bq = cb[u];
-                sh->leave = bx[u];
+        for (int t = 0; t < CH; ++t) {
+            if (wave * len + lane + 64 * t == q && lane + 64 * t < len) {
+                sh->aq = a[t];
+                sh->c_bq = cb[t];
+                sh->leave = bx[t];
             }
         }
         __syncthreads();
@@ -416,19 +420,26 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
     }
 
     // s_y = c_B_new . E_q (v4:354) with c_B_new[q] = c_p (v4:340)
-    double sy = 0.0;
-    if (in_regs) {
+    for (int s = wave; s < NSLICE; s += WAVES) {
+        double acc = 0.0;
+        if (in_regs) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t i = (int64_t)u * BLOCK + tid;
-            if (i < m) sy = fma((i == q) ? c_p : cb[u], eta_entry(a[u], i, q, aq), sy);
+            for (int t = 0; t < CH; ++t) {
+                const int64_t k = lane + 64 * t, i = s * len + k;
+                if (k < len && i < m) acc = fma((i == q) ? c_p : cb[t], eta_entry(a[t], i, q, aq), acc);
+            }
+        } else {
+            for (int64_t k = lane; k < len; k += 64) {
+                const int64_t i = s * len + k;
+                if (i < m) acc = fma((i == q) ? c_p : P.c_B[i], eta_entry(ld_agent(&a_new[i]), i, q, aq), acc);
+            }
         }
-    } else {
-        for (int64_t i = tid; i < m; i += BLOCK)
-            sy = fma((i == q) ? c_p : P.c_B[i], eta_entry(ld_agent(&a_new[i]), i, q, aq), sy);
+        const double v = wave_sum(acc);
+        if (lane == 0) part[s] = v;
     }
     tm = tail_mark(P, 1, tm);
-    sy = block_sum<BLOCK>(sy, sums);
+    __syncthreads();
+    const double sy = block_dot_finish(part);
     tm = tail_mark(P, 2, tm);
 
     if (tid == 0) {

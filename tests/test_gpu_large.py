@@ -1,0 +1,95 @@
+"""GPU: the large-size code paths (chunked tail, big LDS y, global-y pricing)
+and the BASELINE configurations C4/C5 through size-independent invariants.
+
+Tolerances as in test_gpu_parity.py; at C4/C5 the oracle cannot run a window
+in test time, so the checks are B^-1 B = I on sampled basis columns (columns
+regenerated on the host from the seeded generator), x_b = B^-1 b, z = c_B.x_b,
+x_b >= 0 and e_j ~ 0 on basic columns.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def test_every_geometry_bit_identical(spx):
+    """Register tail (16 waves, L <= 4096), chunked tail (fewer waves), LDS-y
+    and global-y pricing, every rows-per-wave: the same bits."""
+    m, n, seed, k = 1100, 3300, 4, 150
+    runs = []
+    for kw in [dict(), dict(update_block=256), dict(update_block=512, update_rows=2), dict(global_y=True),
+               dict(price_block=256, global_y=True), dict(update_block=1024, update_rows=4)]:
+        with spx.Context(m=m, n=n, seed=seed, **kw) as ctx:
+            st, piv = ctx.iterate(k)
+            s = ctx.state(binv=True)
+            s["z"] = ctx.objective()
+            runs.append((kw, piv, s))
+    kw0, piv0, s0 = runs[0]
+    assert piv0 == k
+    for kw, piv, s in runs[1:]:
+        assert piv == piv0, kw
+        for key in ("b_ixs", "x_b", "y", "binv"):
+            assert np.array_equal(s[key], s0[key]), (kw, key)
+        assert s["z"] == s0["z"], kw
+
+
+def test_mid_size_against_oracle(spx, oracle):
+    """m=6000 (chunked tail, L=6016) against the CPU restatement."""
+    m, n, seed, k = 6000, 9000, 2, 40
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, max_iter=k, want_state=True, trace_cap=k)
+    with spx.Context(A, b, c) as ctx:
+        ps, qs = [], []
+        for _ in range(k):
+            p, e, opt = ctx.price()
+            q, st = ctx.pivot()
+            ps.append(p)
+            qs.append(q)
+        s = ctx.state(binv=True)
+    assert ps == list(ref.trace_p) and qs == list(ref.trace_q)
+    assert _rel(s["x_b"], ref.x_b) <= 1e-9
+    assert _rel(s["y"], ref.y) <= 1e-9
+    assert _rel(s["binv"], ref.binv) <= 1e-9
+
+
+def _check_invariants(spx, oracle, m, n, seed, k, ncols=24):
+    with spx.Context(m=m, n=n, seed=seed) as ctx:
+        st, piv = ctx.iterate(k)
+        assert st == spx.SolveStatus.MaxIter and piv == k
+        s = ctx.state(binv=True)
+        z = ctx.objective()
+        e = ctx.reduced_costs()
+    b = (n - m) / 4.0 * (1.0 + oracle.uniform_np(seed, 2, np.arange(m, dtype=np.uint64)))
+    c = np.zeros(n)
+    c[: n - m] = oracle.uniform_np(seed, 3, np.arange(n - m, dtype=np.uint64))
+    rows = np.linspace(0, m - 1, ncols).astype(np.int64)
+    Bcols = np.stack([oracle.column_np(m, n, seed, int(s["b_ixs"][i])) for i in rows], axis=1)
+    I = s["binv"] @ Bcols
+    E = np.zeros_like(I)
+    E[rows, np.arange(len(rows))] = 1.0
+    assert np.max(np.abs(I - E)) < 1e-9
+    assert _rel(s["binv"] @ b, s["x_b"]) < 1e-10
+    assert abs(z - float(c[s["b_ixs"]] @ s["x_b"])) <= 1e-10 * abs(z)
+    assert np.all(s["x_b"] > -1e-9)
+    assert np.max(np.abs(e[s["b_ixs"]])) < 1e-9  # basic columns price to zero
+    assert len(set(s["b_ixs"].tolist())) == m
+
+
+def test_c4_invariants(spx, oracle):
+    """C4 (m=4096, n=131072): 127k priced columns per iteration."""
+    _check_invariants(spx, oracle, 4096, 131072, 0, 40)
+
+
+def test_c5_invariants(spx, oracle):
+    """C5 (m=16384, n=65536): y in 128 KiB of LDS, B^-1 2.1 GB x 2."""
+    _check_invariants(spx, oracle, 16384, 65536, 0, 30, ncols=16)
+
+
+def test_global_y_large_m(spx, oracle):
+    """m=20000: y no longer fits LDS, pricing reads it from global memory."""
+    _check_invariants(spx, oracle, 20000, 21000, 1, 12, ncols=8)
