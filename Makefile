@@ -46,3 +46,9 @@ variant:
 	  -DSPX_NT_BSTORE=$(word 3,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
 	  -c $(SRC)/spx_kernels.hip -o $(BUILD)/v$(NT)/spx_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/v$(NT)/libsimplex.so $(BUILD)/v$(NT)/spx_kernels.o $(BUILD)/spx_api.o $(LDFLAGS)
+
+# in-place vs ping-pong B^-1 storage: make pingpong
+pingpong:
+	@mkdir -p $(BUILD)/pp
+	$(HIPCC) $(HIPFLAGS) -DSPX_INPLACE=0 -c $(SRC)/spx_kernels.hip -o $(BUILD)/pp/spx_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/pp/libsimplex.so $(BUILD)/pp/spx_kernels.o $(BUILD)/spx_api.o $(LDFLAGS)

@@ -203,7 +203,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.ns = x->ns;
     P.eps = x->opts.eps;
     SPX_TRY(x->alloc(&P.B0, (size_t)(m * L)));
-    SPX_TRY(x->alloc(&P.B1, (size_t)(m * L)));
+    if (kernels_inplace())
+        P.B1 = P.B0;
+    else
+        SPX_TRY(x->alloc(&P.B1, (size_t)(m * L)));
+    SPX_TRY(x->alloc(&P.rbuf, (size_t)L));
     SPX_TRY(x->alloc(&P.alpha0, (size_t)L));
     SPX_TRY(x->alloc(&P.alpha1, (size_t)L));
     SPX_TRY(x->alloc(&P.y0, (size_t)L));
@@ -247,9 +251,12 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
 
     UpdateCfg& uc = x->ucfg;
     int ub = x->opts.update_block;
-    if (!(ub == 256 || ub == 512 || ub == 1024)) ub = 1024;
+    // measured (tools/itbench.py): 16 waves x 1 row at m <= 8192 (C3: 1024x1),
+    // 8 waves x 2 rows beyond (C5: 512x2, 4.3 GB streamed per launch)
+    const bool big_m = m > 8192;
+    if (!(ub == 256 || ub == 512 || ub == 1024)) ub = big_m ? 512 : 1024;
     int rows = x->opts.update_rows;
-    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = 1;
+    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = big_m ? 2 : 1;
     if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
     uc.block = ub;
     uc.rows = rows;
@@ -278,7 +285,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
 int do_reset(spx_ctx* x) {
     const size_t mb = (size_t)(x->m * x->L) * sizeof(double);
     HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
-    HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
+    if (x->P.B1 != x->P.B0) HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
     HIP_TRY(launch_reset(x->P, x->stream));

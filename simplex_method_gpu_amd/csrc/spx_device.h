@@ -5,9 +5,11 @@
 //   A      L x n, column-major (column j at A + j*L; rows m..L-1 zero).  The
 //          reference's D = [-c; A] copy (v4:248,278-279) is not built: pricing
 //          reads A and c directly.
-//   B[2]   m x L, ROW-major B^-1 (the reference is column-major, v4:59-60), two
-//          buffers: the update kernel of pass `it` reads S = B[it&1] and writes
-//          B[(it+1)&1].
+//   B      m x L, ROW-major B^-1 S (the reference is column-major, v4:59-60),
+//          updated in place by k_update (SPX_INPLACE=1, default; the ping-pong
+//          variant B0/B1 is a build option kept for A/B measurements).
+//   rbuf   L: the pending pivot row, staged by k_price (k_update overwrites
+//          row q while every wave still needs it).
 //
 // Deferred pivot state.  The last pivot (it-1) is kept in factored form and
 // applied by the kernels that stream the data anyway:
@@ -87,6 +89,7 @@ struct Params {
     double* x_b;
     double* c_B;
     const double* zeros;   // L zeros (the "pivot row" before the first pivot)
+    double* rbuf;          // staged pivot row (in-place B^-1 storage)
     int64_t* b_ixs;
     int32_t* nb_list;
     int32_t* nb_pos;       // n entries, -1 when basic or not owned

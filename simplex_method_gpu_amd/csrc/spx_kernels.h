@@ -19,6 +19,7 @@ struct UpdateCfg {
     int grid;   // ceil(m / (block / 64 * rows))
 };
 
+bool kernels_inplace();  // B^-1 updated in place (one buffer) or ping-pong
 hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu);
 hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);

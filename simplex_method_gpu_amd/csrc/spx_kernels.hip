@@ -47,6 +47,13 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #define SPX_NT_BSTORE 1 // update writes of B_new
 #endif
 
+// B^-1 storage: 1 = one buffer updated in place (the pivot row the stream
+// needs is staged into P.rbuf by k_price); 0 = ping-pong between B0 and B1.
+#ifndef SPX_INPLACE
+#define SPX_INPLACE 1
+#endif
+bool kernels_inplace() { return SPX_INPLACE != 0; }
+
 template <int NT>
 __device__ __forceinline__ dbl2 ld2(const dbl2* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -118,29 +125,10 @@ __device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
     return o;
 }
 
-// s_x = r.b (v4:347) in a canonical order independent of the launch geometry:
-// NSLICE contiguous slices of the padded vectors, lane-strided pairs inside a
-// slice, slices summed in index order.  Each wave computes the slices
-// s = wave, wave + WAVES, ... into part[s]; call block_dot_finish after a
-// barrier.
+// Slice partial sums (NSLICE contiguous slices of a padded vector, each wave
+// lane-strided within its slices, slices added in index order): the canonical,
+// geometry-independent order of the tail's s_y dot product.
 constexpr int NSLICE = 16;
-template <int WAVES>
-__device__ __forceinline__ void block_dot_slices(const double* r, const double* b, int64_t L, double* part) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t len = (L >> 1) / NSLICE;  // L is a multiple of 128
-    for (int s = wave; s < NSLICE; s += WAVES) {
-        const dbl2* r2 = reinterpret_cast<const dbl2*>(r) + s * len;
-        const dbl2* b2 = reinterpret_cast<const dbl2*>(b) + s * len;
-        double a0 = 0.0, a1 = 0.0;
-        for (int64_t k = lane; k < len; k += 64) {
-            const dbl2 x = r2[k], z = b2[k];
-            a0 = fma(x.x, z.x, a0);
-            a1 = fma(x.y, z.y, a1);
-        }
-        const double v = wave_sum(a0 + a1);
-        if (lane == 0) part[s] = v;
-    }
-}
 __device__ __forceinline__ double block_dot_finish(const double* part) {
     double s = part[0];
 #pragma unroll
@@ -175,7 +163,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const double s_y = st->s_y;
     const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
     dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
-    const dbl2* rr = reinterpret_cast<const dbl2*>(upd_y ? ((it & 1) ? P.B1 : P.B0) + st->q * L : P.zeros);
+    const dbl2* rr = reinterpret_cast<const dbl2*>(
+        upd_y ? ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L : P.zeros);
+#if SPX_INPLACE
+    // stage the pending pivot row for k_update, whose in-place stream
+    // overwrites row q while every wave still reads it
+    if (it > 0 && blockIdx.x == 1 % gridDim.x) {
+        const dbl2* rq = reinterpret_cast<const dbl2*>(P.B0 + st->q * L);
+        dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
+        for (int64_t k = tid; k < L2; k += BLOCK) rb[k] = rq[k];
+    }
+#endif
     if constexpr (LDS_Y) {
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
         for (int64_t k = tid; k < L2; k += BLOCK) {
@@ -343,7 +341,7 @@ struct UpdLds {
 // L <= 4096 the alpha / c_B / b_ixs loads are issued together with the
 // partial loads and row q's scalars are broadcast through LDS from the lane
 // that loaded them; otherwise they are loaded after q.  s_y's dot product
-// uses the canonical slice order of block_dot_slices (geometry-independent).
+// uses the canonical NSLICE slice order (geometry-independent).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
                             bool y_was_pending, const double* a_new, unsigned char* smem) {
@@ -429,9 +427,21 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
                 if (k < len && i < m) acc = fma((i == q) ? c_p : cb[t], eta_entry(a[t], i, q, aq), acc);
             }
         } else {
-            for (int64_t k = lane; k < len; k += 64) {
-                const int64_t i = s * len + k;
-                if (i < m) acc = fma((i == q) ? c_p : P.c_B[i], eta_entry(ld_agent(&a_new[i]), i, q, aq), acc);
+            for (int64_t k0 = 0; k0 < len; k0 += 64 * CH) {  // loads batched, then used in order
+                double av[CH], cv[CH];
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int64_t k = k0 + lane + 64 * t, i = s * len + k;
+                    if (k < len && i < m) {
+                        av[t] = ld_agent(&a_new[i]);
+                        cv[t] = P.c_B[i];
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int64_t k = k0 + lane + 64 * t, i = s * len + k;
+                    if (k < len && i < m) acc = fma((i == q) ? c_p : cv[t], eta_entry(av[t], i, q, aq), acc);
+                }
             }
         }
         const double v = wave_sum(acc);
@@ -505,24 +515,36 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t it = st->iter;
     const int par = (int)(it & 1);
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
+#if SPX_INPLACE
+    double* S = P.B0;
+    const dbl2* src = reinterpret_cast<const dbl2*>(S);
+    dbl2* dst = reinterpret_cast<dbl2*>(S);
+#else
     const double* S = par ? P.B1 : P.B0;
     const dbl2* __restrict__ src = reinterpret_cast<const dbl2*>(S);
     dbl2* __restrict__ dst = reinterpret_cast<dbl2*>(par ? P.B0 : P.B1);
+#endif
     const double* a_prev = par ? P.alpha1 : P.alpha0;  // alpha of pivot it-1
     double* a_new = par ? P.alpha0 : P.alpha1;
     // the pending pivot it-1: r = S[q,:], E from a_prev and aq
     const bool pend = it > 0;
     const int64_t qp = st->q;
     const double aqp = st->aq;
+#if SPX_INPLACE
+    const double* rrow = pend ? P.rbuf : P.zeros;
+#else
     const double* rrow = pend ? S + qp * L : P.zeros;
+#endif
     const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(rrow);
     const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
     const bool upd_x = st->xb_applied < it;
     const bool y_was_pending = st->y_applied < it;
 
-    // s_x = r.b for the deferred x_b update: slice partials now, sum after the stream
-    double* slices = reinterpret_cast<double*>(smem + Lds::slices);
-    if (upd_x) block_dot_slices<WAVES>(rrow, P.b, L, slices);
+    // s_x = r.b (v4:347) for the deferred x_b update is accumulated inside the
+    // row stream (every wave streams all of r; lane-strided, k ascending, then
+    // a 64-lane butterfly: the same bits in every wave and in k_flush)
+    const dbl2* __restrict__ bp = reinterpret_cast<const dbl2*>(P.b);
+    double sxa = 0.0;
 
     const int64_t row0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
     const int nvalid = (int)((row0 >= m) ? 0 : ((m - row0 < R) ? (m - row0) : R));
@@ -537,16 +559,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         constexpr int U = (R >= 4) ? 2 : 4;
         int64_t k = lane;
         for (; k + (U - 1) * 64 < L2; k += U * 64) {
-            dbl2 rv[U], av[U], bv[U][R];
+            dbl2 rv[U], av[U], bb[U], bv[U][R];
 #pragma unroll
             for (int t = 0; t < U; ++t) {
                 rv[t] = rp[k + t * 64];
                 av[t] = ap[k + t * 64];
+                bb[t] = bp[k + t * 64];
 #pragma unroll
                 for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
             }
 #pragma unroll
             for (int t = 0; t < U; ++t) {
+                sxa = fma(rv[t].x, bb[t].x, sxa);
+                sxa = fma(rv[t].y, bb[t].y, sxa);
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     dbl2 nv;
@@ -559,7 +584,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             }
         }
         for (; k < L2; k += 64) {
-            const dbl2 rv = rp[k], av = ap[k];
+            const dbl2 rv = rp[k], av = ap[k], bb = bp[k];
+            sxa = fma(rv.x, bb.x, sxa);
+            sxa = fma(rv.y, bb.y, sxa);
 #pragma unroll
             for (int u = 0; u < R; ++u) {
                 const dbl2 bv = src[base + u * L2 + k];
@@ -573,7 +600,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
     } else if (nvalid > 0) {
         for (int64_t k = lane; k < L2; k += 64) {
-            const dbl2 rv = rp[k], av = ap[k];
+            const dbl2 rv = rp[k], av = ap[k], bb = bp[k];
+            sxa = fma(rv.x, bb.x, sxa);
+            sxa = fma(rv.y, bb.y, sxa);
             for (int u = 0; u < nvalid; ++u) {
                 const dbl2 bv = src[base + u * L2 + k];
                 dbl2 nv;
@@ -586,8 +615,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
     }
 
-    __syncthreads();  // slice partials of s_x
-    const double s_x = upd_x ? block_dot_finish(slices) : 0.0;
+    const double s_x = (upd_x && nvalid > 0) ? wave_sum(sxa) : 0.0;
 
     // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
     // (compute_theta, v4:199-208) and the wave's argmin
@@ -642,13 +670,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 // ---------------------------------------------------------------------------
 // Applies the pending y and x_b updates of the last pivot (one workgroup).
 __global__ __launch_bounds__(1024) void k_flush(Params P) {
-    constexpr int BLOCK = 1024, WAVES = BLOCK / 64;
-    __shared__ double slices[NSLICE];
+    constexpr int BLOCK = 1024;
     DevState* st = P.st;
     const int tid = threadIdx.x;
     const int64_t it = st->iter, L = P.L, L2 = L >> 1, m = P.m;
     if (it == 0) return;
-    const double* S = (it & 1) ? P.B1 : P.B0;
+    const double* S = (SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1;
     const double* r = S + st->q * L;
     const bool upd_y = st->y_applied < it, upd_x = st->xb_applied < it;
     if (upd_y) {
@@ -658,9 +685,15 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
         for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(st->s_y, r2[k], yin[k]);
     }
     if (upd_x) {
-        block_dot_slices<WAVES>(r, P.b, L, slices);
-        __syncthreads();
-        const double s_x = block_dot_finish(slices);
+        // s_x exactly as k_update's row stream accumulates it (every wave alike)
+        const dbl2* r2 = reinterpret_cast<const dbl2*>(r);
+        const dbl2* b2 = reinterpret_cast<const dbl2*>(P.b);
+        double sxa = 0.0;
+        for (int64_t k = tid & 63; k < L2; k += 64) {
+            sxa = fma(r2[k].x, b2[k].x, sxa);
+            sxa = fma(r2[k].y, b2[k].y, sxa);
+        }
+        const double s_x = wave_sum(sxa);
         const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
         const int64_t q = st->q;
         const double aq = st->aq;
@@ -680,7 +713,7 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
 __global__ void k_materialize(Params P, double* out) {
     const DevState* st = P.st;
     const int64_t it = st->iter;
-    const double* S = (it & 1) ? P.B1 : P.B0;
+    const double* S = (SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1;
     const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
     const int64_t q = st->q;
     const double aq = st->aq;
