@@ -1,6 +1,6 @@
 """Benchmark: dense revised-simplex iterations/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--m 4096 --n 16384]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C2|C4|C5 | --m M --n N]
 
 A *step* is one simplex iteration (pricing over the non-basic columns, entering
 MINLOC, fused B^-1 rank-1 update + FTRAN, ratio test, x_b / y update) on the
@@ -8,15 +8,19 @@ seeded dense random LP of SURVEY.md §8(d) (default C3: m=4096, n=16384, fp64),
 with A, b, c generated directly in HBM.  W untimed iterations, then exactly K
 timed ones between barriers + device syncs; rank 0 prints one JSON line.
 
-Multi-GPU (torchrun, one process per GPU): pricing columns are sharded over the
-ranks with an RCCL all-gather MINLOC per iteration, B^-1 is replicated, so the
-whole job still does one iteration per step (strong scaling on a fixed LP).
+Multi-GPU (torch.distributed.run, one process per GPU): pricing columns are
+sharded over the ranks with an RCCL all-gather MINLOC per iteration, B^-1 is
+replicated, so the job does one iteration per step ("strong" scaling on a
+fixed LP); `pricing` reports the aggregate pricing throughput (all ranks'
+algorithmic pricing bytes / max-over-ranks of pricing kernel + MINLOC time).
 
-roofline: the pricing kernel (dominant: 60 % of algorithmic bytes at C3),
-algorithmic bytes = 8*(m+1)*(non-basic columns priced) per launch, duration
-from hipEvents recorded by the kernel dispatch itself (hipExtLaunchKernel) on
-the library's stream over the timed region.  cpu_baseline: the oracle
-(oracle/simplex_oracle.c, OpenMP) on a bounded sample of the same workload.
+roofline: the pricing kernel (dominant: 60 % of the algorithmic bytes at C3),
+algorithmic bytes = 8*(m+1)*(non-basic columns priced on this rank) per launch,
+duration from hipEvents recorded by the kernel dispatch itself
+(hipExtLaunchKernel) on the library's stream over the event-timed window;
+traffic = rocprofv3 PMC bytes per launch (profiles/traffic_rNN.json).
+cpu_baseline: the oracle (oracle/simplex_oracle.c, OpenMP) on a bounded sample
+of the same workload (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -30,6 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CONFIGS = {"C2": (1024, 4096), "C3": (4096, 16384), "C4": (4096, 131072), "C5": (16384, 65536)}
+METRIC = "simplex iterations/sec on dense m=4096 n=16384 fp64; achieved HBM GB/s"
 
 
 def parse():
@@ -37,17 +43,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--m", type=int, default=4096)
-    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--update-rows", type=int, default=0)
+    ap.add_argument("--update-block", type=int, default=0)
     ap.add_argument("--price-block", type=int, default=0)
     ap.add_argument("--graph-batch", type=int, default=0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    m, n = CONFIGS[a.config or "C3"]
+    a.m = a.m or m
+    a.n = a.n or n
+    return a
 
 
 def main():
@@ -58,9 +70,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -70,8 +81,8 @@ def main():
 
     def make(timing):
         ctx = spx.Context(m=m, n=n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
-                          update_rows=args.update_rows, price_block=args.price_block,
-                          graph_batch=args.graph_batch)
+                          update_rows=args.update_rows, update_block=args.update_block,
+                          price_block=args.price_block, graph_batch=args.graph_batch)
         if world > 1:
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
@@ -82,17 +93,25 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def max_over_ranks(v):
+    def reduce_max(vals):
         if world == 1:
-            return v
-        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+            return list(vals)
+        t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return t.tolist()
 
-    def timed_window(ctx):
+    def reduce_sum(vals):
+        if world == 1:
+            return list(vals)
+        t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.tolist()
+
+    def timed_window(ctx, events):
         ctx.iterate(args.warmup)
-        if ctx.info()["local_nonbasic"] < 0:
-            raise RuntimeError("bad state")
+        if events:
+            ctx.pass_times()  # drop the warmup's events
+        info0 = ctx.info()
         _, piv0 = ctx.iterate(0)
         barrier()
         torch.cuda.synchronize()
@@ -100,58 +119,48 @@ def main():
         st, piv1 = ctx.iterate(args.steps)
         torch.cuda.synchronize()
         barrier()
-        dt = max_over_ranks(time.perf_counter() - t0)
-        return dt, piv1 - piv0, st
+        dt = reduce_max([time.perf_counter() - t0])[0]
+        pt = ctx.pass_times() if events else None
+        info1 = ctx.info()
+        return dt, piv1 - piv0, pt, 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"])
 
-    # --- timed region with per-kernel hipEvents (eager dispatch)
+    # (1) event-timed window: per-kernel durations recorded by the dispatches
     ctx = make(timing=True)
-    info = ctx.info()
-    ctx.iterate(args.warmup)
-    ctx.kernel_times()  # reset the event pools after warmup
-    _, piv0 = ctx.iterate(0)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    st, piv1 = ctx.iterate(args.steps)
-    torch.cuda.synchronize()
-    barrier()
-    dt = max_over_ranks(time.perf_counter() - t0)
-    kt = ctx.kernel_times()
-    info_end = ctx.info()
+    dt_e, piv_e, pt, nb_local = timed_window(ctx, True)
     ctx.close()
-    pivots = piv1 - piv0
-
-    # --- the same window replayed from captured hipGraphs (no events)
+    # (2) the same window replayed from captured hipGraphs (single rank) or
+    #     launched eagerly with RCCL (multi-rank), no events
     ctx = make(timing=False)
-    dt_g, pivots_g, st_g = timed_window(ctx)
+    dt_g, piv_g, _, _ = timed_window(ctx, False)
     ctx.close()
 
-    # use the faster dispatch mode for `value`; the event-timed run gives the roofline
-    if pivots_g > 0 and dt_g / pivots_g < dt / max(pivots, 1):
-        best_dt, best_piv, mode = dt_g, pivots_g, "hipGraph replay"
+    if piv_g > 0 and dt_g / piv_g <= dt_e / max(piv_e, 1):
+        best_dt, best_piv = dt_g, piv_g
+        mode = "hipGraph replay" if world == 1 else "eager + RCCL all-gather"
     else:
-        best_dt, best_piv, mode = dt, pivots, "eager + hipExtLaunchKernel events"
+        best_dt, best_piv, mode = dt_e, piv_e, "eager + hipExtLaunchKernel events"
     value = best_piv / best_dt if best_dt > 0 else 0.0
 
-    # algorithmic bytes; non-basic count is constant per rank
-    # on average — use the mean of window start/end for this rank's pricing
-    nb_local = 0.5 * (info["local_nonbasic"] + info_end["local_nonbasic"])
-    price_bytes = 8.0 * (m + 1) * nb_local
+    passes = max(pt["passes"], 1)
+    price_ms = pt["price_ms"] / passes
+    minloc_ms = pt["price_minloc_ms"] / passes
+    update_ms = pt["update_ms"] / passes
+    price_ms_max, minloc_ms_max, update_ms_max = reduce_max([price_ms, minloc_ms, update_ms])
+    price_bytes = 8.0 * (m + 1) * nb_local  # this rank's launch
+    price_bytes_all = reduce_sum([price_bytes])[0]
     update_bytes = 16.0 * m * m
-    price_ms = kt["price_ms"] / max(kt["price_launches"], 1)
-    update_ms = kt["update_ms"] / max(kt["update_launches"], 1)
     price_gbs = price_bytes / (price_ms * 1e-3) / 1e9 if price_ms > 0 else 0.0
     update_gbs = update_bytes / (update_ms * 1e-3) / 1e9 if update_ms > 0 else 0.0
-    b_alg = 8.0 * ((m + 1) * (n - m) + 2.0 * m * m)  # whole-iteration, all ranks
+    b_alg = 8.0 * ((m + 1) * (n - m) + 2.0 * m * m)  # one iteration, whole job
 
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("m") == m and tj.get("n") == n:
+            if tj.get("m") == m and tj.get("n") == n and world == 1:
                 traffic = tj.get("price_hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
 
     cpu = None
@@ -160,7 +169,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "simplex iterations/sec on dense m=4096 n=16384 fp64; achieved HBM GB/s",
+            "metric": METRIC,
             "value": value,
             "unit": "iterations/s",
             "n_gpus": world,
@@ -173,16 +182,16 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded generator of SURVEY.md §8(d), generated in HBM)",
             "config": {
-                "workload": f"dense random LP m={m} n={n} seed={args.seed}, Dantzig revised simplex, "
-                            f"explicit B^-1",
+                "workload": f"dense random LP m={m} n={n} seed={args.seed}, Dantzig revised simplex with "
+                            f"explicit B^-1 (one step = one pivot)",
                 "m": m, "n": n, "seed": args.seed,
-                "parallelism": (f"pricing column-sharded x{world} (RCCL all-gather MINLOC), "
-                                "B^-1 replicated") if world > 1 else "single GPU",
+                "parallelism": (f"pricing column-sharded x{world} (RCCL all-gather MINLOC), B^-1 replicated"
+                                if world > 1 else "single GPU"),
                 "dispatch": mode,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_price (pricing GEMV + entering argmin)",
+                "kernel": "k_price (pricing GEMV + entering argmin), rank 0",
                 "achieved": price_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -197,8 +206,15 @@ def main():
                 "iteration": {"algorithmic_bytes": b_alg,
                               "achieved_GBps": b_alg * value / 1e9,
                               "frac": b_alg * value / 1e9 / HBM_PEAK_GBS,
-                              "event_timed_ms_per_step": 1e3 * dt / max(pivots, 1),
-                              "graph_ms_per_step": 1e3 * dt_g / max(pivots_g, 1)},
+                              "event_timed_ms_per_step": 1e3 * dt_e / max(piv_e, 1),
+                              "undisturbed_ms_per_step": 1e3 * dt_g / max(piv_g, 1)},
+            },
+            "pricing": {
+                "bytes_all_ranks": price_bytes_all,
+                "max_rank_price_ms": price_ms_max,
+                "max_rank_price_plus_minloc_ms": minloc_ms_max,
+                "throughput_GBps": price_bytes_all / (minloc_ms_max * 1e-3) / 1e9 if minloc_ms_max > 0 else 0.0,
+                "max_rank_update_ms": update_ms_max,
             },
             "cpu_baseline": cpu,
         }
@@ -217,7 +233,7 @@ def cpu_baseline(m, n, seed, budget_s):
     A, b, c = oracle.generate(m, n, seed)
     t1, d1 = oracle.time_iterations(A, b, c, 2, threads)
     per = t1 / max(d1, 1)
-    k = int(max(3, min(500, budget_s / max(per, 1e-6))))
+    k = int(max(3, min(2000, budget_s / max(per, 1e-6))))
     sec, done = oracle.time_iterations(A, b, c, k, threads)
     return {"value": done / sec, "unit": "iterations/s", "cores": threads, "kind": "port",
             "sample": f"{done} iterations from the slack basis of the same m={m} n={n} LP "

@@ -150,13 +150,21 @@ int spx_objective(spx_ctx* ctx, double* z);
 int spx_kernel_times(spx_ctx* ctx, double* price_ms, int64_t* price_launches,
                      double* update_ms, int64_t* update_launches);
 
+/* With SPX_FLAG_TIMING: device milliseconds summed since the last call (resets)
+ * of out[0] the pricing kernel, out[1] pricing + the cross-rank MINLOC
+ * exchange (RCCL all-gather; == out[0] at one rank), out[2] the update kernel;
+ * passes = timed passes. */
+int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
+
 /* With SPX_FLAG_STAMPS: microseconds summed since the last call of, per
  * kernel, the body (earliest workgroup start -> last workgroup's ticket) and
  * the last-workgroup tail (final reduction; for the update kernel also E_q,
  * r, x_b, y and the basis bookkeeping).  out[0..3] = price body, price tail,
  * update body, update tail; out[4..8] = update-tail sub-phases (partials ->
- * q, row-q loads + E/r/dots, block sum, x_b/y stores, bookkeeping).  Resets. */
-#define SPX_PHASES 9
+ * q, s_y dot, block sum, bookkeeping, -); out[9..12] = update prologue
+ * (earliest workgroup start -> earliest row stream start), update drain
+ * (latest stream end -> last ticket), price prologue, price drain.  Resets. */
+#define SPX_PHASES 13
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
 /* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this

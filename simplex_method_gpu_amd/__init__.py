@@ -217,12 +217,20 @@ class Context:
 
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""
-        out = (ctypes.c_double * 9)()
+        out = (ctypes.c_double * 13)()
         check(self._L.spx_phase_times(self._h, out))
         return {"price_body_us": out[0], "price_tail_us": out[1],
                 "update_body_us": out[2], "update_tail_us": out[3],
-                "tail_partials_us": out[4], "tail_rowq_us": out[5], "tail_blocksum_us": out[6],
-                "tail_stores_us": out[7], "tail_bookkeeping_us": out[8]}
+                "tail_partials_us": out[4], "tail_sy_us": out[5], "tail_blocksum_us": out[6],
+                "tail_bookkeeping_us": out[7], "update_prologue_us": out[9], "update_drain_us": out[10],
+                "price_prologue_us": out[11], "price_drain_us": out[12]}
+
+    def pass_times(self):
+        """Event-timed sums (timing=True): pricing kernel, pricing + MINLOC
+        exchange, update kernel (ms), and the number of timed passes."""
+        out, n = (ctypes.c_double * 3)(), ctypes.c_int64()
+        check(self._L.spx_pass_times(self._h, out, ctypes.byref(n)))
+        return {"price_ms": out[0], "price_minloc_ms": out[1], "update_ms": out[2], "passes": n.value}
 
     def info(self):
         m, n, ld, nb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

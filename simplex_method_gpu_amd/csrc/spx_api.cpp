@@ -111,6 +111,7 @@ struct spx_ctx {
     // per-kernel timing
     bool timing = false;
     std::vector<hipEvent_t> ev_price, ev_update;  // pairs (start, stop)
+    std::vector<hipEvent_t> ev_xend;              // after the MINLOC exchange
     size_t n_price = 0, n_update = 0;
 
     int64_t pivots = 0;
@@ -160,6 +161,8 @@ const char* spx_status_string(int32_t s) {
 }  // extern "C"
 
 namespace {
+
+int reset_stamps(spx_ctx* x);
 
 int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (opts) x->opts = *opts; else spx_default_opts(&x->opts);
@@ -266,9 +269,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
     if (x->opts.flags & SPX_FLAG_STAMPS) {
-        SPX_TRY(x->alloc(&P.stamps, 16));
-        const unsigned long long init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
-        HIP_TRY(hipMemcpy(P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
+        SPX_TRY(x->alloc(&P.stamps, 32));
+        SPX_TRY(reset_stamps(x));
     }
     SPX_TRY(x->alloc(&x->send, 1));
     SPX_TRY(x->alloc(&x->recv, (size_t)G));
@@ -314,6 +316,11 @@ int enqueue_pass(spx_ctx* x, bool timed) {
                 x->ev_update.push_back(e);
             }
         }
+        if (x->ev_xend.size() < x->n_price + 1) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            x->ev_xend.push_back(e);
+        }
         p0 = x->ev_price[2 * x->n_price];
         p1 = x->ev_price[2 * x->n_price + 1];
         u0 = x->ev_update[2 * x->n_update];
@@ -326,6 +333,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
         NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry), ncclUint8, x->comm, x->stream));
     }
+    if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
     return SPX_OK;
 }
@@ -357,6 +365,13 @@ int read_state(spx_ctx* x) {
 int flush(spx_ctx* x) {
     if (x->stepped_price) return fail(SPX_ERR_STATE, "state readback between spx_price and spx_pivot");
     HIP_TRY(launch_flush(x->P, x->stream));
+    return SPX_OK;
+}
+
+int reset_stamps(spx_ctx* x) {
+    unsigned long long init[32] = {0};
+    init[0] = init[4] = init[16] = init[20] = ~0ull;  // running minima
+    HIP_TRY(hipMemcpy(x->P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
     return SPX_OK;
 }
 
@@ -450,6 +465,7 @@ void spx_destroy(spx_ctx* x) {
     if (x->ev_recv) (void)hipEventDestroy(x->ev_recv);
     for (hipEvent_t e : x->ev_price) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_update) (void)hipEventDestroy(e);
+    for (hipEvent_t e : x->ev_xend) (void)hipEventDestroy(e);
     if (x->comm) (void)ncclCommDestroy(x->comm);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->st_host) (void)hipHostFree(x->st_host);
@@ -645,6 +661,30 @@ int spx_pivot(spx_ctx* x, int64_t* q, int32_t* status) {
     return SPX_OK;
 }
 
+int spx_pass_times(spx_ctx* x, double out[3], int64_t* passes) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    double tp = 0.0, tx = 0.0, tu = 0.0;
+    for (size_t i = 0; i < x->n_price; ++i) {
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, x->ev_price[2 * i], x->ev_price[2 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, x->ev_price[2 * i], x->ev_xend[i]));
+        tp += a;
+        tx += b;
+    }
+    for (size_t i = 0; i < x->n_update; ++i) {
+        float a = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, x->ev_update[2 * i], x->ev_update[2 * i + 1]));
+        tu += a;
+    }
+    out[0] = tp;
+    out[1] = tx;
+    out[2] = tu;
+    if (passes) *passes = (int64_t)x->n_price;
+    x->n_price = x->n_update = 0;
+    return SPX_OK;
+}
+
 int spx_kernel_times(spx_ctx* x, double* price_ms, int64_t* np, double* update_ms, int64_t* nu) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     HIP_TRY(hipStreamSynchronize(x->stream));
@@ -670,18 +710,19 @@ int spx_kernel_times(spx_ctx* x, double* price_ms, int64_t* np, double* update_m
 int spx_phase_times(spx_ctx* x, double out[SPX_PHASES]) {
     if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
     if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
-    unsigned long long h[16];
+    unsigned long long h[32];
     HIP_TRY(hipStreamSynchronize(x->stream));
     HIP_TRY(hipMemcpy(h, x->P.stamps, sizeof(h), hipMemcpyDeviceToHost));
     for (int k = 0; k < 5; ++k) out[4 + k] = h[8 + k] * 0.01;
-    HIP_TRY(hipMemset(x->P.stamps + 8, 0, 8 * sizeof(unsigned long long)));
+    out[9] = h[18] * 0.01;   // update prologue
+    out[10] = h[19] * 0.01;  // update drain
+    out[11] = h[22] * 0.01;  // price prologue
+    out[12] = h[23] * 0.01;  // price drain
     out[0] = h[1] * 0.01;  // 100 MHz ticks -> us
     out[1] = h[2] * 0.01;
     out[2] = h[5] * 0.01;
     out[3] = h[6] * 0.01;
-    const unsigned long long init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
-    HIP_TRY(hipMemcpy(x->P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
-    return SPX_OK;
+    return reset_stamps(x);
 }
 
 int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb, double* bp, double* bu) {

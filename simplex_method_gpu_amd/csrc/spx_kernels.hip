@@ -91,13 +91,30 @@ __device__ __forceinline__ unsigned long long rtime() { return __builtin_amdgcn_
 __device__ __forceinline__ void stamp_start(unsigned long long* slot) {
     if (slot && threadIdx.x == 0) atomicMin(&slot[0], rtime());
 }
-__device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned long long t_tail) {
+// Stream window per launch: slot[S+0] = earliest wave stream start, slot[S+1]
+// = latest wave stream end; the tail adds prologue (earliest stream start -
+// earliest workgroup start) to slot[S+2] and drain (last ticket - latest
+// stream end) to slot[S+3].
+__device__ __forceinline__ void stamp_stream(unsigned long long* s, bool begin) {
+    if (s && threadIdx.x == 0) {  // one atomic per workgroup (wave 0 as its proxy)
+        if (begin) atomicMin(&s[0], rtime());
+        else atomicMax(&s[1], rtime());
+    }
+}
+__device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned long long t_tail,
+                                           unsigned long long* win) {
     if (slot && threadIdx.x == 0) {
         const unsigned long long t_end = rtime();
         const unsigned long long t0 = __hip_atomic_load(&slot[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&slot[1], t_tail - t0);
         atomicAdd(&slot[2], t_end - t_tail);
         __hip_atomic_store(&slot[0], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(&win[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long e = __hip_atomic_load(&win[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&win[2], b - t0);
+        atomicAdd(&win[3], t_tail - e);
+        __hip_atomic_store(&win[0], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&win[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 // Sub-phase marks inside the update tail: slot 8+k accumulates the ticks since
@@ -157,35 +174,47 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    // current y = ybuf + s_y r when the last pivot's y update is pending
+    // current y = ybuf + s_y r when the last pivot's y update is pending.
+    // Workgroup 0 also persists that y and (in-place B^-1) stages the pending
+    // pivot row r for k_update.  Loads are batched YB deep per thread so the
+    // fill is one memory round trip, not one per element.
     const int64_t it = st->iter;
+    const bool pend = it > 0;
     const bool upd_y = st->y_applied < it;
     const double s_y = st->s_y;
     const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
     dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
     const dbl2* rr = reinterpret_cast<const dbl2*>(
-        upd_y ? ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L : P.zeros);
-#if SPX_INPLACE
-    // stage the pending pivot row for k_update, whose in-place stream
-    // overwrites row q while every wave still reads it
-    if (it > 0 && blockIdx.x == 1 % gridDim.x) {
-        const dbl2* rq = reinterpret_cast<const dbl2*>(P.B0 + st->q * L);
-        dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
-        for (int64_t k = tid; k < L2; k += BLOCK) rb[k] = rq[k];
-    }
-#endif
-    if constexpr (LDS_Y) {
+        pend ? ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L : P.zeros);
+    const bool wg0 = blockIdx.x == 0;
+    const bool stage_r = SPX_INPLACE && pend && wg0;
+    constexpr int YB = 8;
+    if (LDS_Y || wg0) {
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
-        for (int64_t k = tid; k < L2; k += BLOCK) {
-            const dbl2 v = upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
-            yl[k] = v;
-            if (upd_y && blockIdx.x == 0) yout[k] = v;  // persisted once (flipped by k_update's tail)
+        dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
+        for (int64_t k0 = 0; k0 < L2; k0 += (int64_t)YB * BLOCK) {
+            dbl2 yv[YB], rv[YB];
+#pragma unroll
+            for (int u = 0; u < YB; ++u) {
+                const int64_t k = k0 + (int64_t)u * BLOCK + tid;
+                if (k < L2) {
+                    yv[u] = yin[k];
+                    if (upd_y || stage_r) rv[u] = rr[k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < YB; ++u) {
+                const int64_t k = k0 + (int64_t)u * BLOCK + tid;
+                if (k < L2) {
+                    const dbl2 v = upd_y ? y_apply(s_y, rv[u], yv[u]) : yv[u];
+                    if constexpr (LDS_Y) yl[k] = v;
+                    if (upd_y && wg0) yout[k] = v;  // flipped in by k_update's tail
+                    if (stage_r) rb[k] = rv[u];
+                }
+            }
         }
-        __syncthreads();
-    } else {
-        if (upd_y && blockIdx.x == 0)
-            for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(s_y, rr[k], yin[k]);
     }
+    if constexpr (LDS_Y) __syncthreads();
     auto Y = [&](int64_t k) -> dbl2 {
         if constexpr (LDS_Y) return reinterpret_cast<const dbl2*>(ys)[k];
         else return upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
@@ -194,6 +223,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int nb = st->nb_count;
     double best = INFINITY;
     int64_t bj = INT64_MAX;
+    unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
+    stamp_stream(win, true);
     for (int idx = blockIdx.x * WAVES + wave; idx < nb; idx += gridDim.x * WAVES) {
         const int64_t j = P.nb_list[idx];
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
@@ -220,6 +251,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (argmin_better(e, j, best, bj)) { best = e; bj = j; }
     }
 
+    stamp_stream(win, false);
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
     if (lane == 0) red[wave] = ArgMinEntry{best, bj};
     __syncthreads();
@@ -261,7 +293,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         *P.price_out = t;
         st_agent(&st->ticket_price, 0u);
     }
-    stamp_tail(slot, t_tail);
+    stamp_tail(slot, t_tail, win);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,6 +587,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         acc[u] = 0.0;
     }
     const int64_t base = row0 * L2;
+    unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
+    stamp_stream(win, true);
     if (nvalid == R) {
         constexpr int U = (R >= 4) ? 2 : 4;
         int64_t k = lane;
@@ -615,6 +649,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
     }
 
+    stamp_stream(win, false);
     const double s_x = (upd_x && nvalid > 0) ? wave_sum(sxa) : 0.0;
 
     // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
@@ -662,7 +697,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
     update_tail<BLOCK>(P, st, p, min_e, it, y_was_pending, a_new, smem);
-    stamp_tail(slot, t_tail);
+    stamp_tail(slot, t_tail, win);
 }
 
 // ---------------------------------------------------------------------------

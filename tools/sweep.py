@@ -28,7 +28,7 @@ def run(m, n, k, warm, **kw):
         "price_us": 1e3 * kt["price_ms"] / nl, "update_us": 1e3 * kt["update_ms"] / nl,
         "price_body_us": ph["price_body_us"] / nl, "price_tail_us": ph["price_tail_us"] / nl,
         "update_body_us": ph["update_body_us"] / nl, "update_tail_us": ph["update_tail_us"] / nl,
-        **{k: v / nl for k, v in ph.items() if k.startswith("tail_")},
+        **{k: v / nl for k, v in ph.items() if k.startswith("tail_") or "prologue" in k or "drain" in k},
         "update_GBps": 16.0 * m * m / (kt["update_ms"] / nl * 1e-3) / 1e9,
         "price_GBps": 8.0 * (m + 1) * info["local_nonbasic"] / (kt["price_ms"] / nl * 1e-3) / 1e9,
     }
