@@ -9,10 +9,12 @@ with A, b, c generated directly in HBM.  W untimed iterations, then exactly K
 timed ones between barriers + device syncs; rank 0 prints one JSON line.
 
 Multi-GPU (torch.distributed.run, one process per GPU): pricing columns are
-sharded over the ranks with an RCCL all-gather MINLOC per iteration, B^-1 is
-replicated, so the job does one iteration per step ("strong" scaling on a
-fixed LP); `pricing` reports the aggregate pricing throughput (all ranks'
-algorithmic pricing bytes / max-over-ranks of pricing kernel + MINLOC time).
+sharded over the ranks with an RCCL all-gather MINLOC per iteration and B^-1 is
+row-sharded (ceil(m/N) rows per rank; the ratio-test all-gather carries each
+rank's candidate pivot row), or replicated with --replicated.  The job does one
+iteration per step ("strong" scaling on a fixed LP); `pricing` reports the
+aggregate pricing throughput (all ranks' algorithmic pricing bytes /
+max-over-ranks of pricing kernel + MINLOC time).
 
 roofline: the pricing kernel (dominant: 60 % of the algorithmic bytes at C3),
 algorithmic bytes = 8*(m+1)*(non-basic columns priced on this rank) per launch,
@@ -55,6 +57,8 @@ def parse():
     ap.add_argument("--update-block", type=int, default=0)
     ap.add_argument("--price-block", type=int, default=0)
     ap.add_argument("--graph-batch", type=int, default=0)
+    ap.add_argument("--replicated", action="store_true",
+                    help="N > 1: keep B^-1 replicated instead of row-sharded (SPX_FLAG_ROW_SHARD)")
     a = ap.parse_args()
     m, n = CONFIGS[a.config or "C3"]
     a.m = a.m or m
@@ -82,7 +86,8 @@ def main():
     def make(timing):
         ctx = spx.Context(m=m, n=n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
                           update_rows=args.update_rows, update_block=args.update_block,
-                          price_block=args.price_block, graph_batch=args.graph_batch)
+                          price_block=args.price_block, graph_batch=args.graph_batch,
+                          row_shard=(world > 1 and not args.replicated))
         if world > 1:
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
@@ -185,7 +190,9 @@ def main():
                 "workload": f"dense random LP m={m} n={n} seed={args.seed}, Dantzig revised simplex with "
                             f"explicit B^-1 (one step = one pivot)",
                 "m": m, "n": n, "seed": args.seed,
-                "parallelism": (f"pricing column-sharded x{world} (RCCL all-gather MINLOC), B^-1 replicated"
+                "parallelism": ((f"pricing column-sharded x{world} (RCCL all-gather MINLOC), " +
+                                 ("B^-1 replicated" if args.replicated else
+                                  "B^-1 row-sharded (pivot row in a 2nd all-gather)"))
                                 if world > 1 else "single GPU"),
                 "dispatch": mode,
             },

@@ -79,6 +79,12 @@ typedef struct spx_opts {
 #define SPX_FLAG_STAMPS 2 /* in-kernel phase stamps (spx_phase_times); diagnostic */
 #define SPX_FLAG_GLOBAL_Y 4 /* pricing reads y from global memory instead of LDS
                                (automatic when L*8 bytes do not fit in LDS)   */
+#define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
+                                (ceil(m/nranks) rows each) instead of
+                                replicated; one extra all-gather per pass
+                                carries the pivot row.  Readback functions
+                                then gather x_b over the communicator
+                                (collective: every rank must call them).     */
 
 void spx_default_opts(spx_opts* opts);
 
@@ -106,6 +112,12 @@ int spx_attach_comm(spx_ctx* ctx, const uint8_t id[SPX_COMM_ID_BYTES]);
  * way the sharded path is validated on one GPU).  status/pivots: rank 0's. */
 int spx_group_iterate(spx_ctx** ctxs, int32_t G, int64_t k, int32_t* status,
                       int64_t* pivots);
+
+/* Row-sharded groups (SPX_FLAG_ROW_SHARD, no communicator): flush every
+ * member and copy each member's x_b rows to all members, so per-context
+ * readback (spx_get_state x_b / spx_objective / spx_solve) is complete.
+ * spx_get_state's B^-1 then still holds only the member's own rows. */
+int spx_group_sync(spx_ctx** ctxs, int32_t G);
 
 /* Back to the slack basis (keeps A, b, c). */
 int spx_reset(spx_ctx* ctx);

@@ -23,12 +23,13 @@ import numpy as np
 from ._lib import SimplexError, SpxOpts, check, load
 
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
-           "shard_range", "minloc_merge", "group_iterate",
+           "shard_range", "minloc_merge", "group_iterate", "group_sync",
            "SimplexError", "FLAG_TIMING"]
 
 FLAG_TIMING = 1
 FLAG_STAMPS = 2
 FLAG_GLOBAL_Y = 4
+FLAG_ROW_SHARD = 8
 
 
 class SolveStatus(IntEnum):
@@ -96,6 +97,12 @@ def group_iterate(ctxs, k: int):
     return SolveStatus(st.value), piv.value
 
 
+def group_sync(ctxs):
+    """Row-sharded groups: flush every member and exchange x_b rows (spx_group_sync)."""
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    check(load().spx_group_sync(arr, len(ctxs)))
+
+
 def comm_unique_id() -> bytes:
     buf = (ctypes.c_uint8 * 128)()
     check(load().spx_comm_unique_id(buf))
@@ -110,7 +117,7 @@ class Context:
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
-                 global_y: bool = False):
+                 global_y: bool = False, row_shard: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -118,7 +125,7 @@ class Context:
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
         o.update_block = update_block
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
-                   | (FLAG_GLOBAL_Y if global_y else 0))
+                   | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)

@@ -43,6 +43,7 @@ SIGNATURES = {
     "spx_attach_comm": (ctypes.c_int, [_p, _p]),
     "spx_reset": (ctypes.c_int, [_p]),
     "spx_group_iterate": (ctypes.c_int, [_p, _i32, _i64, _p, _p]),
+    "spx_group_sync": (ctypes.c_int, [_p, _i32]),
     "spx_solve": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _p]),
     "spx_iterate": (ctypes.c_int, [_p, _i64, _p, _p]),
     "spx_price": (ctypes.c_int, [_p, _p, _p, _p]),

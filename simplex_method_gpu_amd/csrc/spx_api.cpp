@@ -106,7 +106,10 @@ struct spx_ctx {
     int batch = 0;
 
     // in-process group exchange
-    hipEvent_t ev_sent = nullptr, ev_recv = nullptr;
+    hipEvent_t ev_sent = nullptr, ev_recv = nullptr, ev_sent2 = nullptr, ev_recv2 = nullptr;
+    // row-sharded B^-1
+    int64_t mb = 0;
+    unsigned char* rs_recv = nullptr;
 
     // per-kernel timing
     bool timing = false;
@@ -205,17 +208,24 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.L = L;
     P.ns = x->ns;
     P.eps = x->opts.eps;
-    SPX_TRY(x->alloc(&P.B0, (size_t)(m * L)));
-    if (kernels_inplace())
+    // row shard of B^-1 (SPX_FLAG_ROW_SHARD with nranks > 1): rows
+    // [r0, r0 + mloc), ping-pong storage; otherwise all rows, in place
+    P.row_shard = (G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD)) ? 1 : 0;
+    x->mb = P.row_shard ? (m + G - 1) / G : m;
+    P.r0 = P.row_shard ? std::min<int64_t>(m, (int64_t)r * x->mb) : 0;
+    P.mloc = P.row_shard ? std::min<int64_t>(m, P.r0 + x->mb) - P.r0 : m;
+    if (P.row_shard && P.mloc <= 0) return fail(SPX_ERR_ARG, "row sharding needs m >= nranks rows per rank");
+    SPX_TRY(x->alloc(&P.B0, (size_t)(std::max<int64_t>(P.mloc, 1) * L)));
+    if (kernels_inplace() && !P.row_shard)
         P.B1 = P.B0;
     else
-        SPX_TRY(x->alloc(&P.B1, (size_t)(m * L)));
+        SPX_TRY(x->alloc(&P.B1, (size_t)(std::max<int64_t>(P.mloc, 1) * L)));
     SPX_TRY(x->alloc(&P.rbuf, (size_t)L));
     SPX_TRY(x->alloc(&P.alpha0, (size_t)L));
     SPX_TRY(x->alloc(&P.alpha1, (size_t)L));
     SPX_TRY(x->alloc(&P.y0, (size_t)L));
     SPX_TRY(x->alloc(&P.y1, (size_t)L));
-    SPX_TRY(x->alloc(&P.x_b, (size_t)L));
+    SPX_TRY(x->alloc(&P.x_b, (size_t)std::max<int64_t>(L, (int64_t)G * x->mb)));  // G*mb: in-place all-gather
     SPX_TRY(x->alloc(&P.c_B, (size_t)L));
     double* zeros = nullptr;
     SPX_TRY(x->alloc(&zeros, (size_t)L));
@@ -264,7 +274,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     uc.block = ub;
     uc.rows = rows;
     const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
-    uc.grid = (int)std::max<int64_t>(1, (m + rows_per_wg - 1) / rows_per_wg);
+    uc.grid = (int)std::max<int64_t>(1, (P.mloc + rows_per_wg - 1) / rows_per_wg);
 
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
@@ -274,6 +284,15 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     }
     SPX_TRY(x->alloc(&x->send, 1));
     SPX_TRY(x->alloc(&x->recv, (size_t)G));
+    if (P.row_shard) {
+        P.rs_stride = (int64_t)sizeof(RsHeader) + 8 * L;
+        unsigned char *sb = nullptr, *rb = nullptr;
+        SPX_TRY(x->alloc(&sb, (size_t)P.rs_stride));
+        SPX_TRY(x->alloc(&rb, (size_t)(P.rs_stride * G)));
+        P.rs_send = sb;
+        P.rs_recv = rb;
+        x->rs_recv = rb;
+    }
     P.price_out = x->send;
     P.price_in = (G == 1) ? x->send : x->recv;
     P.nin = G;
@@ -285,7 +304,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
 }
 
 int do_reset(spx_ctx* x) {
-    const size_t mb = (size_t)(x->m * x->L) * sizeof(double);
+    const size_t mb = (size_t)(std::max<int64_t>(x->P.mloc, 1) * x->L) * sizeof(double);
     HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
     if (x->P.B1 != x->P.B0) HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
@@ -335,6 +354,10 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
+    if (x->P.row_shard) {  // ratio-test all-gather (header + candidate row), then finalise
+        NCCL_TRY(ncclAllGather(x->P.rs_send, x->rs_recv, (size_t)x->P.rs_stride, ncclUint8, x->comm, x->stream));
+        HIP_TRY(launch_finalize_rs(x->P, x->stream));
+    }
     return SPX_OK;
 }
 
@@ -372,6 +395,14 @@ int reset_stamps(spx_ctx* x) {
     unsigned long long init[32] = {0};
     init[0] = init[4] = init[16] = init[20] = ~0ull;  // running minima
     HIP_TRY(hipMemcpy(x->P.stamps, init, sizeof(init), hipMemcpyHostToDevice));
+    return SPX_OK;
+}
+
+// Row-sharded storage with a communicator: every rank's x_b rows to all
+// ranks (in-place all-gather of ceil(m/G)-row slices).  Collective.
+int gather_xb(spx_ctx* x) {
+    if (!x->P.row_shard || !x->comm_ready) return SPX_OK;
+    NCCL_TRY(ncclAllGather(x->P.x_b + x->P.r0, x->P.x_b, (size_t)x->mb, ncclFloat64, x->comm, x->stream));
     return SPX_OK;
 }
 
@@ -461,8 +492,8 @@ void spx_destroy(spx_ctx* x) {
     if (x->stream) (void)hipStreamSynchronize(x->stream);
     if (x->graph_exec) (void)hipGraphExecDestroy(x->graph_exec);
     if (x->graph) (void)hipGraphDestroy(x->graph);
-    if (x->ev_sent) (void)hipEventDestroy(x->ev_sent);
-    if (x->ev_recv) (void)hipEventDestroy(x->ev_recv);
+    for (hipEvent_t e : {x->ev_sent, x->ev_recv, x->ev_sent2, x->ev_recv2})
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_price) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_update) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_xend) (void)hipEventDestroy(e);
@@ -519,10 +550,13 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
         if (x->comm_ready) return fail(SPX_ERR_STATE, "group contexts must not have a communicator");
         if (x->m != cs[0]->m || x->n != cs[0]->n) return fail(SPX_ERR_ARG, "group shape mismatch");
         if (x->status != cs[0]->status || x->pivots != cs[0]->pivots) return fail(SPX_ERR_STATE, "group out of step");
+        if (x->P.row_shard != cs[0]->P.row_shard) return fail(SPX_ERR_ARG, "group mixes storage modes");
         if (!x->ev_sent) {
             HIP_TRY(hipSetDevice(x->device));
             HIP_TRY(hipEventCreateWithFlags(&x->ev_sent, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&x->ev_recv, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&x->ev_sent2, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&x->ev_recv2, hipEventDisableTiming));
         }
     }
     if (cs[0]->status == SPX_STATUS_MAX_ITER && k > 0) {
@@ -547,11 +581,35 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 }
                 HIP_TRY(hipEventRecord(x->ev_recv, x->stream));
             }
-            for (int g = 0; g < G; ++g) {  // replicated fused update; next pricing waits for every reader
+            const bool rs = cs[0]->P.row_shard != 0;
+            for (int g = 0; g < G; ++g) {  // fused update; next pricing waits for every reader
                 spx_ctx* x = cs[g];
                 HIP_TRY(hipSetDevice(x->device));
                 HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
-                for (int h = 0; h < G; ++h) HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv, 0));
+                if (rs) HIP_TRY(hipEventRecord(x->ev_sent2, x->stream));
+                else
+                    for (int h = 0; h < G; ++h) HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv, 0));
+            }
+            if (rs) {
+                for (int h = 0; h < G; ++h) {  // ratio-test all-gather: headers + candidate rows
+                    spx_ctx* x = cs[h];
+                    HIP_TRY(hipSetDevice(x->device));
+                    for (int g = 0; g < G; ++g) {
+                        HIP_TRY(hipStreamWaitEvent(x->stream, cs[g]->ev_sent2, 0));
+                        HIP_TRY(hipMemcpyAsync(x->rs_recv + g * x->P.rs_stride, cs[g]->P.rs_send,
+                                               (size_t)x->P.rs_stride, hipMemcpyDefault, x->stream));
+                    }
+                    HIP_TRY(hipEventRecord(x->ev_recv2, x->stream));
+                }
+                for (int g = 0; g < G; ++g) {
+                    spx_ctx* x = cs[g];
+                    HIP_TRY(hipSetDevice(x->device));
+                    HIP_TRY(launch_finalize_rs(x->P, x->stream));
+                    for (int h = 0; h < G; ++h) {
+                        HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv, 0));
+                        HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv2, 0));
+                    }
+                }
             }
         }
         for (int g = 0; g < G; ++g) {
@@ -568,9 +626,28 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
     return SPX_OK;
 }
 
+int spx_group_sync(spx_ctx** cs, int32_t G) {
+    if (!cs || G < 1) return fail(SPX_ERR_ARG, "bad group");
+    for (int g = 0; g < G; ++g) {
+        if (!cs[g] || cs[g]->opts.nranks != G || cs[g]->opts.rank != g) return fail(SPX_ERR_ARG, "bad group member");
+        HIP_TRY(hipSetDevice(cs[g]->device));
+        SPX_TRY(flush(cs[g]));
+        HIP_TRY(hipStreamSynchronize(cs[g]->stream));
+    }
+    if (!cs[0]->P.row_shard) return SPX_OK;
+    for (int h = 0; h < G; ++h)
+        for (int g = 0; g < G; ++g)
+            if (g != h && cs[g]->P.mloc > 0)
+                HIP_TRY(hipMemcpyAsync(cs[h]->P.x_b + cs[g]->P.r0, cs[g]->P.x_b + cs[g]->P.r0,
+                                       (size_t)cs[g]->P.mloc * 8, hipMemcpyDefault, cs[h]->stream));
+    for (int h = 0; h < G; ++h) HIP_TRY(hipStreamSynchronize(cs[h]->stream));
+    return SPX_OK;
+}
+
 int spx_objective(spx_ctx* x, double* z) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     SPX_TRY(flush(x));
+    SPX_TRY(gather_xb(x));
     HIP_TRY(launch_objective(x->P, x->stream));
     SPX_TRY(read_state(x));
     if (z) *z = x->st_host->z;
@@ -582,6 +659,7 @@ int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     const size_t mb = (size_t)x->m * 8;
     SPX_TRY(flush(x));
+    SPX_TRY(gather_xb(x));
     SPX_TRY(read_state(x));  // y_buf after the flush
     if (x_b) HIP_TRY(hipMemcpyAsync(x_b, x->P.x_b, mb, hipMemcpyDeviceToHost, x->stream));
     if (b_ixs) HIP_TRY(hipMemcpyAsync(b_ixs, x->P.b_ixs, mb, hipMemcpyDeviceToHost, x->stream));
@@ -589,8 +667,13 @@ int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_
     if (c_b) HIP_TRY(hipMemcpyAsync(c_b, x->P.c_B, mb, hipMemcpyDeviceToHost, x->stream));
     if (binv) {
         double* tmp = nullptr;
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)(x->m * x->L) * 8, x->stream));
+        const size_t rows = (size_t)std::max<int64_t>(x->m, (int64_t)x->opts.nranks * x->mb);
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), rows * x->L * 8, x->stream));
+        if (x->P.row_shard) HIP_TRY(hipMemsetAsync(tmp, 0, rows * x->L * 8, x->stream));
         HIP_TRY(launch_materialize(x->P, tmp, x->stream));
+        if (x->P.row_shard && x->comm_ready)
+            NCCL_TRY(ncclAllGather(tmp + x->P.r0 * x->L, tmp, (size_t)(x->mb * x->L), ncclFloat64, x->comm,
+                                   x->stream));
         HIP_TRY(hipMemcpy2DAsync(binv, mb, tmp, (size_t)x->L * 8, mb, (size_t)x->m, hipMemcpyDeviceToHost, x->stream));
         HIP_TRY(hipFreeAsync(tmp, x->stream));
     }

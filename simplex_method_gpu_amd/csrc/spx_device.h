@@ -46,6 +46,21 @@ struct alignas(16) UpdPartial {
     double theta;
     int64_t idx;
     int64_t nonpos;
+    double T;  // row-sharded mode: sum of c_B[i] * alpha_i over the workgroup's rows
+};
+
+// Row-sharded mode: what each rank contributes to the ratio-test all-gather —
+// its local leaving candidate plus that row of B^-1_new, so every rank
+// receives the pivot row without a host-side broadcast root.  Followed in
+// memory by L doubles (the row); entries are rs_stride bytes apart.
+struct alignas(16) RsHeader {
+    double theta;    // local min ratio (first index on ties)
+    int64_t idx;     // its global row, INT64_MAX if none
+    int64_t nonpos;  // local count of alpha_i <= 0
+    double T;        // sum over own rows of c_B[i] * alpha_i
+    double a_w;      // alpha at idx
+    double cb_w;     // c_B at idx
+    int64_t bix_w;   // b_ixs at idx
     int64_t pad;
 };
 
@@ -102,6 +117,13 @@ struct Params {
     int32_t nin;
     UpdPartial* upd_partials;
     DevState* st;
+    // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
+    // global rows [r0, r0 + mloc) of B^-1, stored as B0/B1 (mloc x L ping-pong)
+    int32_t row_shard;
+    int64_t r0, mloc;
+    unsigned char* rs_send;        // RsHeader + row
+    const unsigned char* rs_recv;  // nin entries of rs_stride bytes
+    int64_t rs_stride;
     // diagnostics (SPX_FLAG_STAMPS): per kernel {min WG start, sum body, sum tail}
     // in s_memrealtime ticks (100 MHz); nullptr in normal runs
     unsigned long long* stamps;

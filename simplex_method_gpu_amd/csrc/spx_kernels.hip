@@ -184,10 +184,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const double s_y = st->s_y;
     const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
     dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
+    // the pending pivot row: row q of the stored B^-1 (replicated storage), or
+    // rbuf, staged by k_finalize_rs from the all-gather (row-sharded storage)
     const dbl2* rr = reinterpret_cast<const dbl2*>(
-        pend ? ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L : P.zeros);
+        !pend ? P.zeros
+              : (P.row_shard ? P.rbuf : ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L));
     const bool wg0 = blockIdx.x == 0;
-    const bool stage_r = SPX_INPLACE && pend && wg0;
+    const bool stage_r = SPX_INPLACE && pend && wg0 && !P.row_shard;
     constexpr int YB = 8;
     if (LDS_Y || wg0) {
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
@@ -515,7 +518,11 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
     tm = tail_mark(P, 3, tm);
 }
 
-template <int BLOCK, int R>
+template <int BLOCK>
+__device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
+                               const double* a_new, unsigned char* smem);
+
+template <int BLOCK, int R, bool RS>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
     if (stopped(st)) return;
@@ -547,26 +554,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t it = st->iter;
     const int par = (int)(it & 1);
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
-#if SPX_INPLACE
-    double* S = P.B0;
+    // row-sharded storage always ping-pongs (its tail recomputes the winner
+    // row from the old rows); replicated storage per SPX_INPLACE
+    constexpr bool INPL = SPX_INPLACE && !RS;
+    const double* S = INPL ? P.B0 : (par ? P.B1 : P.B0);
     const dbl2* src = reinterpret_cast<const dbl2*>(S);
-    dbl2* dst = reinterpret_cast<dbl2*>(S);
-#else
-    const double* S = par ? P.B1 : P.B0;
-    const dbl2* __restrict__ src = reinterpret_cast<const dbl2*>(S);
-    dbl2* __restrict__ dst = reinterpret_cast<dbl2*>(par ? P.B0 : P.B1);
-#endif
+    dbl2* dst = reinterpret_cast<dbl2*>(INPL ? P.B0 : (par ? P.B0 : P.B1));
     const double* a_prev = par ? P.alpha1 : P.alpha0;  // alpha of pivot it-1
     double* a_new = par ? P.alpha0 : P.alpha1;
     // the pending pivot it-1: r = S[q,:], E from a_prev and aq
     const bool pend = it > 0;
     const int64_t qp = st->q;
     const double aqp = st->aq;
-#if SPX_INPLACE
-    const double* rrow = pend ? P.rbuf : P.zeros;
-#else
-    const double* rrow = pend ? S + qp * L : P.zeros;
-#endif
+    const double* rrow = !pend ? P.zeros : ((SPX_INPLACE || RS) ? P.rbuf : S + qp * L);
     const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(rrow);
     const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
     const bool upd_x = st->xb_applied < it;
@@ -578,15 +578,18 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const dbl2* __restrict__ bp = reinterpret_cast<const dbl2*>(P.b);
     double sxa = 0.0;
 
-    const int64_t row0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
-    const int nvalid = (int)((row0 >= m) ? 0 : ((m - row0 < R) ? (m - row0) : R));
+    // rows of this wave: local storage rows lr0.., global rows gr0..
+    const int64_t nrows = RS ? P.mloc : m;
+    const int64_t lr0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
+    const int64_t gr0 = (RS ? P.r0 : 0) + lr0;
+    const int nvalid = (int)((lr0 >= nrows) ? 0 : ((nrows - lr0 < R) ? (nrows - lr0) : R));
     double ei[R], acc[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-        ei[u] = (pend && u < nvalid) ? eta_entry(a_prev[row0 + u], row0 + u, qp, aqp) : 0.0;
+        ei[u] = (pend && u < nvalid) ? eta_entry(a_prev[gr0 + u], gr0 + u, qp, aqp) : 0.0;
         acc[u] = 0.0;
     }
-    const int64_t base = row0 * L2;
+    const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
     if (nvalid == R) {
@@ -657,11 +660,13 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     double wbest = INFINITY;
     int64_t wi = INT64_MAX;
     int64_t nonpos = 0;
+    double wT = 0.0;
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         if (u < nvalid) {
             const double a = wave_sum(acc[u]);
-            const int64_t i = row0 + u;
+            const int64_t i = gr0 + u;
+            if constexpr (RS) wT = fma(P.c_B[i], a, wT);
             double xb = P.x_b[i];
             if (upd_x) xb = fma(s_x, ei[u], xb);
             if (lane == 0) {
@@ -677,17 +682,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     drain_vmem();  // every storing wave drains its alpha stores before the barrier
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
-    if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, 0};
+    if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, wT};
     __syncthreads();
     if (tid == 0) {
         UpdPartial w = red[0];
         for (int i = 1; i < WAVES; ++i) {
             if (argmin_better(red[i].theta, red[i].idx, w.theta, w.idx)) { w.theta = red[i].theta; w.idx = red[i].idx; }
             w.nonpos += red[i].nonpos;
+            w.T += red[i].T;
         }
         st_agent(&P.upd_partials[blockIdx.x].theta, w.theta);
         st_agent(&P.upd_partials[blockIdx.x].idx, w.idx);
         st_agent(&P.upd_partials[blockIdx.x].nonpos, w.nonpos);
+        if constexpr (RS) st_agent(&P.upd_partials[blockIdx.x].T, w.T);
         drain_vmem();
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -696,8 +703,151 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     __syncthreads();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
-    update_tail<BLOCK>(P, st, p, min_e, it, y_was_pending, a_new, smem);
+    if constexpr (RS)
+        update_tail_rs<BLOCK>(P, st, it, par, a_prev, a_new, smem);
+    else
+        update_tail<BLOCK>(P, st, p, min_e, it, y_was_pending, a_new, smem);
     stamp_tail(slot, t_tail, win);
+}
+
+// Row-sharded tail (last workgroup of k_update on this rank): the local
+// leaving candidate, the local sum of c_B[i] * alpha_i, and the candidate's
+// row of B^-1_new — recomputed from the old rows exactly as the stream wrote
+// it — into rs_send for the ratio-test all-gather.  No global state changes:
+// k_finalize_rs does them after the exchange.
+template <int BLOCK>
+__device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
+                               const double* a_new, unsigned char* smem) {
+    using Lds = UpdLds<BLOCK>;
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
+    // workgroup partials: argmin (total order), nonpos, and T in a fixed order
+    UpdPartial w{INFINITY, INT64_MAX, 0, 0.0};
+    for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
+        const double th = ld_agent(&P.upd_partials[g].theta);
+        const int64_t i = ld_agent(&P.upd_partials[g].idx);
+        w.nonpos += ld_agent(&P.upd_partials[g].nonpos);
+        w.T += ld_agent(&P.upd_partials[g].T);
+        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double th = __shfl_xor(w.theta, off, 64);
+        const int64_t i = __shfl_xor(w.idx, off, 64);
+        w.nonpos += __shfl_xor(w.nonpos, off, 64);
+        w.T += __shfl_xor(w.T, off, 64);
+        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
+    }
+    if (lane == 0) red[wave] = w;
+    __syncthreads();
+    UpdPartial t = red[0];
+#pragma unroll
+    for (int k = 1; k < WAVES; ++k) {
+        if (argmin_better(red[k].theta, red[k].idx, t.theta, t.idx)) { t.theta = red[k].theta; t.idx = red[k].idx; }
+        t.nonpos += red[k].nonpos;
+        t.T += red[k].T;
+    }
+    RsHeader* h = reinterpret_cast<RsHeader*>(P.rs_send);
+    double* row = reinterpret_cast<double*>(P.rs_send + sizeof(RsHeader));
+    const bool have = t.idx >= P.r0 && t.idx < P.r0 + P.mloc;
+    if (have) {
+        const int64_t i = t.idx, L2 = P.L >> 1;
+        const double e = (it > 0) ? eta_entry(a_prev[i], i, st->q, st->aq) : 0.0;
+        const dbl2* sr = reinterpret_cast<const dbl2*>((par ? P.B1 : P.B0) + (i - P.r0) * P.L);
+        const dbl2* rb = reinterpret_cast<const dbl2*>(it > 0 ? P.rbuf : P.zeros);
+        dbl2* out = reinterpret_cast<dbl2*>(row);
+        for (int64_t k = tid; k < L2; k += BLOCK) {
+            const dbl2 bv = sr[k], rv = rb[k];
+            dbl2 nv;
+            nv.x = fma(e, rv.x, bv.x);
+            nv.y = fma(e, rv.y, bv.y);
+            out[k] = nv;
+        }
+    }
+    if (tid == 0) {
+        h->theta = t.theta;
+        h->idx = have ? t.idx : INT64_MAX;
+        h->nonpos = t.nonpos;
+        h->T = t.T;
+        h->a_w = have ? ld_agent(&a_new[t.idx]) : 0.0;
+        h->cb_w = have ? P.c_B[t.idx] : 0.0;
+        h->bix_w = have ? P.b_ixs[t.idx] : -1;
+        st_agent(&st->ticket_update, 0u);
+    }
+}
+
+// Row-sharded pivot finalisation (one workgroup, after the ratio-test
+// all-gather): global leaving row q = MINLOC over the ranks' headers
+// (v4:324), Unbounded if every alpha_i <= 0 (v4:317-322), the pivot row into
+// rbuf, s_y (v4:352-355; c_B_new.E_q evaluated from the gathered sum
+// T = sum_i c_B[i] alpha_i as -(T - c_Bq alpha_q)/alpha_q + c_p (1/alpha_q - 1),
+// since alpha is distributed), and the basis bookkeeping (v4:339-342).
+__global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
+    DevState* st = P.st;
+    if (stopped(st)) return;
+    const int tid = threadIdx.x;
+    double min_e = INFINITY;
+    int64_t p = INT64_MAX;
+    for (int g = 0; g < P.nin; ++g) {
+        const ArgMinEntry e = P.price_in[g];
+        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
+    }
+    // merge the ranks' ratio-test headers (rank order: deterministic T sum)
+    double th = INFINITY, T = 0.0;
+    int64_t q = INT64_MAX, nonpos = 0;
+    int w = -1;
+    for (int g = 0; g < P.nin; ++g) {
+        const RsHeader* h = reinterpret_cast<const RsHeader*>(P.rs_recv + g * P.rs_stride);
+        if (argmin_better(h->theta, h->idx, th, q)) { th = h->theta; q = h->idx; w = g; }
+        nonpos += h->nonpos;
+        T += h->T;
+    }
+    const int64_t it = st->iter;
+    if (nonpos == P.m || q < 0 || q >= P.m || w < 0) {
+        if (tid == 0) {
+            st->p = p;
+            st->min_e = min_e;
+            st->status = ST_UNBOUNDED;
+        }
+        return;
+    }
+    const RsHeader* hw = reinterpret_cast<const RsHeader*>(P.rs_recv + w * P.rs_stride);
+    const dbl2* row = reinterpret_cast<const dbl2*>(P.rs_recv + w * P.rs_stride + sizeof(RsHeader));
+    dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
+    for (int64_t k = tid; k < (P.L >> 1); k += 256) rb[k] = row[k];
+    if (tid == 0) {
+        const double aq = hw->a_w, c_bq = hw->cb_w, c_p = P.c[p];
+        const int64_t leave = hw->bix_w;
+        const double sy = -(T - c_bq * aq) / aq + c_p * (1.0 / aq - 1.0);
+        // basis bookkeeping (v4:339-342) + non-basic list swap-remove / append
+        P.c_B[q] = c_p;
+        P.b_ixs[q] = p;
+        int cnt = st->nb_count;
+        if (owns_col(P, p)) {
+            const int kp = P.nb_pos[p];
+            const int last = P.nb_list[cnt - 1];
+            P.nb_list[kp] = last;
+            P.nb_pos[last] = kp;
+            P.nb_pos[p] = -1;
+            --cnt;
+        }
+        if (owns_col(P, leave)) {
+            P.nb_list[cnt] = (int32_t)leave;
+            P.nb_pos[leave] = cnt;
+            ++cnt;
+        }
+        st->nb_count = cnt;
+        st->aq = aq;
+        st->s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+        if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
+        st->y_applied = it;
+        st->xb_applied = it;
+        st->p = p;
+        st->q = q;
+        st->min_e = min_e;
+        st->iter = it + 1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -711,7 +861,7 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
     const int64_t it = st->iter, L = P.L, L2 = L >> 1, m = P.m;
     if (it == 0) return;
     const double* S = (SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1;
-    const double* r = S + st->q * L;
+    const double* r = P.row_shard ? P.rbuf : S + st->q * L;
     const bool upd_y = st->y_applied < it, upd_x = st->xb_applied < it;
     if (upd_y) {
         const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
@@ -732,7 +882,8 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
         const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
         const int64_t q = st->q;
         const double aq = st->aq;
-        for (int64_t i = tid; i < m; i += BLOCK) P.x_b[i] = fma(s_x, eta_entry(a_prev[i], i, q, aq), P.x_b[i]);
+        const int64_t i0 = P.row_shard ? P.r0 : 0, i1 = P.row_shard ? P.r0 + P.mloc : m;  // own rows
+        for (int64_t i = i0 + tid; i < i1; i += BLOCK) P.x_b[i] = fma(s_x, eta_entry(a_prev[i], i, q, aq), P.x_b[i]);
     }
     __syncthreads();
     if (tid == 0) {
@@ -744,19 +895,23 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
     }
 }
 
-// true B^-1 = S + E r^T into out (m x L row-major)
+// true B^-1 = S + E r^T into out (m x L row-major; row-sharded: own rows only,
+// at their global positions)
 __global__ void k_materialize(Params P, double* out) {
     const DevState* st = P.st;
     const int64_t it = st->iter;
-    const double* S = (SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1;
+    const bool rs = P.row_shard != 0;
+    const double* S = rs ? ((it & 1) ? P.B1 : P.B0) : ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1);
+    const double* r = rs ? P.rbuf : S + st->q * P.L;
     const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
     const int64_t q = st->q;
     const double aq = st->aq;
-    const int64_t total = P.m * P.L;
+    const int64_t r0 = rs ? P.r0 : 0;
+    const int64_t total = (rs ? P.mloc : P.m) * P.L;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = t / P.L, k = t - i * P.L;
-        out[t] = (it > 0) ? fma(eta_entry(a_prev[i], i, q, aq), S[q * P.L + k], S[t]) : S[t];
+        const int64_t li = t / P.L, k = t - li * P.L, i = r0 + li;
+        out[r0 * P.L + t] = (it > 0) ? fma(eta_entry(a_prev[i], i, q, aq), r[k], S[t]) : S[t];
     }
 }
 
@@ -822,8 +977,8 @@ __global__ void k_reset(Params P) {
     const int64_t m = P.m, n = P.n, L = P.L, ns = P.ns;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t li = t0; li < P.mloc; li += stride) P.B0[li * L + P.r0 + li] = 1.0;  // init_I (v4:182-188)
     for (int64_t i = t0; i < m; i += stride) {
-        P.B0[i * L + i] = 1.0;  // init_I (v4:182-188)
         P.c_B[i] = P.c[ns + i];
         P.x_b[i] = P.b[i];
         P.y0[i] = P.c[ns + i];
@@ -916,14 +1071,25 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
     return hipErrorInvalidValue;
 }
 
-template <int BLOCK, int R>
-static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+template <int BLOCK, int R, bool RS>
+static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = UpdLds<BLOCK>::bytes;
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
-        hipLaunchKernelGGL((k_update<BLOCK, R>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_update<BLOCK, R, RS>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
+    return hipGetLastError();
+}
+
+template <int BLOCK, int R>
+static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    return P.row_shard ? launch_update_k<BLOCK, R, true>(P, grid, s, e0, e1)
+                       : launch_update_k<BLOCK, R, false>(P, grid, s, e0, e1);
+}
+
+hipError_t launch_finalize_rs(const Params& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize_rs, dim3(1), dim3(256), 0, s, P);
     return hipGetLastError();
 }
 
@@ -974,7 +1140,8 @@ hipError_t launch_flush(const Params& P, hipStream_t s) {
 }
 
 hipError_t launch_materialize(const Params& P, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(k_materialize, dim3(grid_for(P.m * P.L, 256)), dim3(256), 0, s, P, out);
+    hipLaunchKernelGGL(k_materialize, dim3(grid_for((P.row_shard ? P.mloc : P.m) * P.L, 256)), dim3(256), 0, s, P,
+                       out);
     return hipGetLastError();
 }
 

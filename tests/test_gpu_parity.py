@@ -243,3 +243,72 @@ def test_shard_group_solves_to_golden_optimum(spx, golden):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("G,m,n,k", [(2, 300, 1200, 150), (3, 257, 771, 120), (8, 512, 2048, 200),
+                                     (4, 1100, 3300, 100), (2, 5000, 7000, 30)])
+def test_row_sharded_group_matches_single_rank(spx, G, m, n, k):
+    """B^-1 row-sharded over G in-process shards (pivot row carried by the
+    ratio-test all-gather): same pivots as one rank; values within 1e-9 (s_y is
+    evaluated from the gathered c_B.alpha sum, a reassociation)."""
+    seed = 13
+    with spx.Context(m=m, n=n, seed=seed) as ref:
+        rst, rpiv = ref.iterate(k)
+        rs = ref.state(binv=True)
+        rz = ref.objective()
+    ctxs = [spx.Context(m=m, n=n, seed=seed, rank=g, nranks=G, row_shard=True) for g in range(G)]
+    try:
+        st, piv = spx.group_iterate(ctxs, k)
+        assert st == rst and piv == rpiv
+        spx.group_sync(ctxs)
+        binv = np.zeros((m, m))
+        mb = (m + G - 1) // G
+        for g, c in enumerate(ctxs):
+            s = c.state(binv=True)
+            assert np.array_equal(s["b_ixs"], rs["b_ixs"])
+            assert _rel(s["x_b"], rs["x_b"]) <= 1e-9
+            assert _rel(s["y"], rs["y"]) <= 1e-9
+            assert abs(c.objective() - rz) <= 1e-9 * abs(rz)
+            binv[g * mb:(g + 1) * mb] = s["binv"][g * mb:(g + 1) * mb]
+        assert _rel(binv, rs["binv"]) <= 1e-9
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_row_sharded_group_solves_to_golden_optimum(spx, golden):
+    case = [c for c in golden["cases"] if c["m"] == 512][0]
+    G = 4
+    ctxs = [spx.Context(m=case["m"], n=case["n"], seed=case["seed"], rank=g, nranks=G, row_shard=True)
+            for g in range(G)]
+    try:
+        st = spx.SolveStatus.MaxIter
+        while st == spx.SolveStatus.MaxIter:
+            st, piv = spx.group_iterate(ctxs, 128)
+        assert st == spx.SolveStatus.OptimumFound and piv == case["oracle_pivots"]
+        spx.group_sync(ctxs)
+        r = ctxs[2].solve(0)
+        assert abs(r.z - case["highs_z"]) <= 1e-9 * abs(case["highs_z"])
+        assert sorted(int(j) for j in r.b_ixs) == case["highs_basis"]
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_row_sharded_unbounded(spx, oracle):
+    m, n = 3, 6
+    A = np.zeros((n, m))
+    A[0] = [-1.0, 0.0, -2.0]
+    A[1] = [1.0, 1.0, 1.0]
+    A[2] = [2.0, 0.5, 1.0]
+    A[3:] = np.eye(m)
+    b = np.array([4.0, 3.0, 5.0])
+    c = np.array([1.0, 0.5, 0.25, 0, 0, 0])
+    o = oracle.solve(A, b, c)
+    ctxs = [spx.Context(A, b, c, rank=g, nranks=3, row_shard=True) for g in range(3)]
+    try:
+        st, piv = spx.group_iterate(ctxs, 20)
+        assert st == spx.SolveStatus.Unbounded and piv == o.pivots
+    finally:
+        for c in ctxs:
+            c.close()

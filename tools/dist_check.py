@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--k", type=int, default=300)
     ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--row-shard", action="store_true")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -34,7 +35,7 @@ def main():
     dev = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
     import simplex_method_gpu_amd as spx
 
-    ctx = spx.Context(m=a.m, n=a.n, seed=a.seed, device=dev, rank=rank, nranks=world)
+    ctx = spx.Context(m=a.m, n=a.n, seed=a.seed, device=dev, rank=rank, nranks=world, row_shard=a.row_shard)
     obj = [spx.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     ctx.attach_comm(obj[0])
