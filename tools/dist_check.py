@@ -5,7 +5,8 @@
 
 Every rank runs the same LP with its pricing shard; rank 0 also runs the
 single-rank solve.  The sharded run must reproduce the single-rank run bit for
-bit (same pivots, b_ixs, x_b, y) on every rank.  Ranks map to devices
+bit (same pivots, b_ixs, x_b, y) on every rank — within 1e-9 with
+--row-shard, where s_y is evaluated from the gathered c_B.alpha sum.  Ranks map to devices
 LOCAL_RANK % device_count, so it also runs (RCCL permitting) with several
 ranks on one GPU.  The out-of-band id exchange uses a gloo group.
 """
@@ -54,11 +55,15 @@ def main():
             rst, rpiv = ref.iterate(a.k)
             rs = ref.state()
             rz = ref.objective()
+        def close(u, v):  # row-sharded storage reassociates s_y: 1e-9 instead of bitwise
+            u, v = np.asarray(u), np.asarray(v)
+            return np.array_equal(u, v) if not a.row_shard else \
+                float(np.max(np.abs(u - v))) <= 1e-9 * max(1.0, float(np.max(np.abs(v))))
+
         for r, d in enumerate(allr):
-            same = (d["status"] == int(rst) and d["pivots"] == rpiv and d["z"] == rz
+            same = (d["status"] == int(rst) and d["pivots"] == rpiv and close([d["z"]], [rz])
                     and d["b_ixs"] == rs["b_ixs"].tolist()
-                    and np.array_equal(np.array(d["x_b"]), rs["x_b"])
-                    and np.array_equal(np.array(d["y"]), rs["y"]))
+                    and close(d["x_b"], rs["x_b"]) and close(d["y"], rs["y"]))
             print(f"rank {r}: status={d['status']} pivots={d['pivots']} z={d['z']!r} identical_to_1rank={same}")
             ok &= same
         print("DIST_CHECK", "PASS" if ok else "FAIL", flush=True)
