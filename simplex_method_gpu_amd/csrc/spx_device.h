@@ -42,11 +42,19 @@ struct alignas(16) ArgMinEntry {
     int64_t idx;
 };
 
+// Ratio-test partial of one k_update workgroup: its leaving candidate (first
+// index on ties) with that row's alpha / c_B / b_ixs, the count of
+// alpha_i <= 0, and T = sum of c_B[i] * alpha_i over its rows — everything
+// the pivot needs, so the last workgroup's tail is one round trip.
 struct alignas(16) UpdPartial {
     double theta;
     int64_t idx;
     int64_t nonpos;
-    double T;  // row-sharded mode: sum of c_B[i] * alpha_i over the workgroup's rows
+    double T;
+    double a_w;
+    double cb_w;
+    int64_t bix_w;
+    int64_t pad;
 };
 
 // Row-sharded mode: what each rank contributes to the ratio-test all-gather —

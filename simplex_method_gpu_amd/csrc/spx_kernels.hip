@@ -142,37 +142,41 @@ __device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
     return o;
 }
 
-// Slice partial sums (NSLICE contiguous slices of a padded vector, each wave
-// lane-strided within its slices, slices added in index order): the canonical,
-// geometry-independent order of the tail's s_y dot product.
-constexpr int NSLICE = 16;
-__device__ __forceinline__ double block_dot_finish(const double* part) {
-    double s = part[0];
-#pragma unroll
-    for (int k = 1; k < NSLICE; ++k) s += part[k];
-    return s;
-}
-
 // ---------------------------------------------------------------------------
 // Pricing + entering argmin
 // ---------------------------------------------------------------------------
 template <int BLOCK, bool LDS_Y>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int idx0 = blockIdx.x * WAVES + wave;
+    // speculative: this wave's first non-basic column, loaded together with the
+    // status word (index clamped into the list; validated against nb_count)
+    const int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
     if (stopped(st)) return;
     unsigned long long* const slot = P.stamps;
     stamp_start(slot);
-    constexpr int WAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t L = P.L;
     const int64_t L2 = L >> 1;
     double* ys = reinterpret_cast<double*>(smem);
     ArgMinEntry* red = reinterpret_cast<ArgMinEntry*>(smem + (LDS_Y ? L * 8 : 0));
     int* s_last = reinterpret_cast<int*>(red + BLOCK);
+    const int nb = st->nb_count;
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the first CH chunks of the first column stay in flight during the y
+    // staging below (the A stream does not wait for the LDS fill)
+    constexpr int CH = 8;
+    const bool pre = idx0 < nb && L2 >= CH * 64;
+    dbl2 v0[CH];
+    if (pre) {
+        const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&c0[lane + u * 64]);
+    }
 
     // current y = ybuf + s_y r when the last pivot's y update is pending.
     // Workgroup 0 also persists that y and (in-place B^-1) stages the pending
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
               : (P.row_shard ? P.rbuf : ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L));
     const bool wg0 = blockIdx.x == 0;
     const bool stage_r = SPX_INPLACE && pend && wg0 && !P.row_shard;
-    constexpr int YB = 8;
+    constexpr int YB = 4;
     if (LDS_Y || wg0) {
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
         dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
@@ -223,16 +227,27 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         else return upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
     };
 
-    const int nb = st->nb_count;
     double best = INFINITY;
     int64_t bj = INT64_MAX;
     unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
-    for (int idx = blockIdx.x * WAVES + wave; idx < nb; idx += gridDim.x * WAVES) {
-        const int64_t j = P.nb_list[idx];
+    // consume the prefetched chunks first (same k order as the loop)
+    double p0 = 0.0, p1 = 0.0;
+    if (pre) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const dbl2 w = Y(lane + u * 64);
+            p0 = fma(v0[u].x, w.x, p0);
+            p1 = fma(v0[u].y, w.y, p1);
+        }
+    }
+    for (int idx = idx0; idx < nb; idx += gridDim.x * WAVES) {
+        const bool first = idx == idx0;
+        const int64_t j = first ? j0 : (int64_t)P.nb_list[idx];
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
-        double a0 = 0.0, a1 = 0.0;
-        int64_t k = lane;
+        const bool cont = first && pre;
+        double a0 = cont ? p0 : 0.0, a1 = cont ? p1 : 0.0;
+        int64_t k = lane + (cont ? CH * 64 : 0);
         for (; k + 7 * 64 < L2; k += 8 * 64) {
             dbl2 v[8];
 #pragma unroll
@@ -318,209 +333,153 @@ __device__ double block_sum(double a, double* sa) {
     return t;
 }
 
+// Merge of ratio-test partials: argmin on (theta, idx) carrying the winner's
+// scalars; nonpos and T summed.  Callers fix the order of the sums.
+__device__ __forceinline__ void upd_merge(UpdPartial& a, const UpdPartial& b) {
+    if (argmin_better(b.theta, b.idx, a.theta, a.idx)) {
+        a.theta = b.theta;
+        a.idx = b.idx;
+        a.a_w = b.a_w;
+        a.cb_w = b.cb_w;
+        a.bix_w = b.bix_w;
+    }
+    a.nonpos += b.nonpos;
+    a.T += b.T;
+}
+__device__ __forceinline__ UpdPartial upd_empty() { return UpdPartial{INFINITY, INT64_MAX, 0, 0.0, 0.0, 0.0, -1, 0}; }
+__device__ __forceinline__ UpdPartial upd_shfl_xor(const UpdPartial& v, int off) {
+    UpdPartial o;
+    o.theta = __shfl_xor(v.theta, off, 64);
+    o.idx = __shfl_xor(v.idx, off, 64);
+    o.nonpos = __shfl_xor(v.nonpos, off, 64);
+    o.T = __shfl_xor(v.T, off, 64);
+    o.a_w = __shfl_xor(v.a_w, off, 64);
+    o.cb_w = __shfl_xor(v.cb_w, off, 64);
+    o.bix_w = __shfl_xor(v.bix_w, off, 64);
+    o.pad = 0;
+    return o;
+}
+
 // Leaving argmin over the k_update workgroup partials + unbounded count
-// (v4:317-325).  Result broadcast to every thread.
+// (v4:317-325), carrying the winner's scalars.  One dependent round trip
+// (the sc1 partial loads); result broadcast to every thread.  The T sum's
+// order is fixed for a given launch geometry.
 template <int BLOCK>
 __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    UpdPartial w{INFINITY, INT64_MAX, 0, 0};
+    UpdPartial w = upd_empty();
     for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
-        const double th = ld_agent(&P.upd_partials[g].theta);
-        const int64_t i = ld_agent(&P.upd_partials[g].idx);
-        const int64_t np = ld_agent(&P.upd_partials[g].nonpos);
-        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
-        w.nonpos += np;
+        const UpdPartial* src = &P.upd_partials[g];
+        UpdPartial v;
+        v.theta = ld_agent(&src->theta);
+        v.idx = ld_agent(&src->idx);
+        v.nonpos = ld_agent(&src->nonpos);
+        v.T = ld_agent(&src->T);
+        v.a_w = ld_agent(&src->a_w);
+        v.cb_w = ld_agent(&src->cb_w);
+        v.bix_w = ld_agent(&src->bix_w);
+        upd_merge(w, v);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const double th = __shfl_xor(w.theta, off, 64);
-        const int64_t i = __shfl_xor(w.idx, off, 64);
-        w.nonpos += __shfl_xor(w.nonpos, off, 64);
-        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
+        // butterfly partner merge in a fixed role order: lower lane's value first
+        const UpdPartial o = upd_shfl_xor(w, off);
+        UpdPartial lo = (lane & off) ? o : w;
+        const UpdPartial hi = (lane & off) ? w : o;
+        upd_merge(lo, hi);
+        w = lo;
     }
     if (lane == 0) red[wave] = w;
     __syncthreads();
     UpdPartial t = red[0];
 #pragma unroll
-    for (int k = 1; k < WAVES; ++k) {
-        if (argmin_better(red[k].theta, red[k].idx, t.theta, t.idx)) { t.theta = red[k].theta; t.idx = red[k].idx; }
-        t.nonpos += red[k].nonpos;
-    }
+    for (int k = 1; k < WAVES; ++k) upd_merge(t, red[k]);
     __syncthreads();
     return t;
 }
-
-struct TailShared {
-    double aq, c_bq;
-    int64_t leave;
-    int64_t pad;
-};
 
 // LDS carve-up of k_update (dynamic, 16-byte aligned pieces)
 template <int BLOCK>
 struct UpdLds {
     static constexpr int WAVES = BLOCK / 64;
-    static constexpr size_t red = 0;                                        // UpdPartial[WAVES]
-    static constexpr size_t shared = red + sizeof(UpdPartial) * WAVES;      // TailShared
-    static constexpr size_t sums = shared + sizeof(TailShared);             // double[WAVES]
-    static constexpr size_t slices = sums + 8 * ((WAVES + 1) / 2 * 2);      // double[NSLICE]
-    static constexpr size_t last = slices + 8 * NSLICE;                     // int
+    static constexpr size_t red = 0;                                    // UpdPartial[WAVES]
+    static constexpr size_t last = red + sizeof(UpdPartial) * WAVES;    // int
     static constexpr size_t bytes = last + 16;
 };
 
-// The last workgroup of k_update: leaving row q, unboundedness (v4:317-325),
-// alpha_q, s_y = c_B_new.E_q + c_p - c_Bq (v4:352-355) and the basis
-// bookkeeping (v4:339-342).  The vector updates themselves are deferred (see
-// spx_device.h), so this is one dependent round trip: with 16 waves and
-// L <= 4096 the alpha / c_B / b_ixs loads are issued together with the
-// partial loads and row q's scalars are broadcast through LDS from the lane
-// that loaded them; otherwise they are loaded after q.  s_y's dot product
-// uses the canonical NSLICE slice order (geometry-independent).
+// y-update scalar (v4:352-355): c_B_new.E_q + c_p - c_Bq with E_i = -alpha_i /
+// alpha_q (i != q), E_q = 1/alpha_q - 1, c_B_new[q] = c_p, evaluated from the
+// gathered T = sum_i c_B[i] alpha_i (so the tail needs no O(m) pass):
+// c_B_new.E_q = -(T - c_Bq alpha_q)/alpha_q + c_p (1/alpha_q - 1).
+__device__ __forceinline__ double y_scalar(double T, double aq, double c_bq, double c_p) {
+    const double sy = -(T - c_bq * aq) / aq + c_p * (1.0 / aq - 1.0);
+    return sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+}
+
+// Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and
+// the deferred pivot state (spx_device.h).  One thread.
+__device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st, int64_t p, int64_t q,
+                                                  int64_t leave, double aq, double s_y, double min_e,
+                                                  int64_t it) {
+    P.c_B[q] = P.c[p];
+    P.b_ixs[q] = p;
+    int cnt = st->nb_count;
+    if (owns_col(P, p)) {
+        const int kp = P.nb_pos[p];
+        const int last = P.nb_list[cnt - 1];
+        P.nb_list[kp] = last;
+        P.nb_pos[last] = kp;
+        P.nb_pos[p] = -1;
+        --cnt;
+    }
+    if (owns_col(P, leave)) {
+        P.nb_list[cnt] = (int32_t)leave;
+        P.nb_pos[leave] = cnt;
+        ++cnt;
+    }
+    st->nb_count = cnt;
+    st->aq = aq;
+    st->s_y = s_y;
+    if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
+    st->y_applied = it;
+    st->xb_applied = it;
+    st->p = p;
+    st->q = q;
+    st->min_e = min_e;
+    st->iter = it + 1;
+}
+
+// The last workgroup of k_update (single rank / replicated B^-1): leaving
+// row q, unboundedness (v4:317-325), alpha_q, s_y and the bookkeeping.  The
+// vector updates are deferred (spx_device.h).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            bool y_was_pending, const double* a_new, unsigned char* smem) {
-    using Lds = UpdLds<BLOCK>;
-    constexpr int WAVES = BLOCK / 64;
-    constexpr int CH = 4;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t m = P.m;
-    const int64_t len = P.L / NSLICE;  // elements per slice
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
-    TailShared* sh = reinterpret_cast<TailShared*>(smem + Lds::shared);
-    double* part = reinterpret_cast<double*>(smem + Lds::slices);
-    const bool in_regs = (WAVES == NSLICE) && (len <= 64 * CH);
-
+                            unsigned char* smem) {
     unsigned long long tm = P.stamps ? rtime() : 0;
-    double a[CH], cb[CH];
-    int64_t bx[CH];
-    if (in_regs) {
-#pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int64_t k = lane + 64 * t, i = wave * len + k;
-            if (k < len && i < m) {
-                a[t] = ld_agent(&a_new[i]);
-                cb[t] = P.c_B[i];
-                bx[t] = P.b_ixs[i];
-            }
-        }
-    }
-    const double c_p = P.c[p];
-    const bool own_p = owns_col(P, p);
-    int cnt = 0, kp = -1, last = -1;
-    if (tid == 0) {
-        cnt = st->nb_count;
-        if (own_p) {
-            kp = P.nb_pos[p];
-            last = P.nb_list[cnt - 1];
-        }
-    }
-
-    const UpdPartial t0 = reduce_update_partials<BLOCK>(P, red);
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
     tm = tail_mark(P, 0, tm);
-    const int64_t q = t0.idx;
-    if (t0.nonpos == m || q < 0 || q >= m) {
+    if (threadIdx.x != 0) return;
+    const int64_t q = t.idx;
+    if (t.nonpos == P.m || q < 0 || q >= P.m) {
         // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no
         // valid candidate (NaN-poisoned x_b) stops the same way.  The deferred
         // state of the previous pivot (q, aq, s_y) is left intact for k_flush.
-        if (tid == 0) {
-            st->p = p;
-            st->min_e = min_e;
-            st->status = ST_UNBOUNDED;
-            st_agent(&st->ticket_update, 0u);
-        }
+        st->p = p;
+        st->min_e = min_e;
+        st->status = ST_UNBOUNDED;
+        st_agent(&st->ticket_update, 0u);
         return;
     }
-    double aq, c_bq;
-    int64_t leave;
-    if (in_regs) {
-#pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            if (wave * len + lane + 64 * t == q && lane + 64 * t < len) {
-                sh->aq = a[t];
-                sh->c_bq = cb[t];
-                sh->leave = bx[t];
-            }
-        }
-        __syncthreads();
-        aq = sh->aq;
-        c_bq = sh->c_bq;
-        leave = sh->leave;
-    } else {
-        aq = ld_agent(&a_new[q]);
-        c_bq = P.c_B[q];
-        leave = P.b_ixs[q];
-    }
-
-    // s_y = c_B_new . E_q (v4:354) with c_B_new[q] = c_p (v4:340)
-    for (int s = wave; s < NSLICE; s += WAVES) {
-        double acc = 0.0;
-        if (in_regs) {
-#pragma unroll
-            for (int t = 0; t < CH; ++t) {
-                const int64_t k = lane + 64 * t, i = s * len + k;
-                if (k < len && i < m) acc = fma((i == q) ? c_p : cb[t], eta_entry(a[t], i, q, aq), acc);
-            }
-        } else {
-            for (int64_t k0 = 0; k0 < len; k0 += 64 * CH) {  // loads batched, then used in order
-                double av[CH], cv[CH];
-#pragma unroll
-                for (int t = 0; t < CH; ++t) {
-                    const int64_t k = k0 + lane + 64 * t, i = s * len + k;
-                    if (k < len && i < m) {
-                        av[t] = ld_agent(&a_new[i]);
-                        cv[t] = P.c_B[i];
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < CH; ++t) {
-                    const int64_t k = k0 + lane + 64 * t, i = s * len + k;
-                    if (k < len && i < m) acc = fma((i == q) ? c_p : cv[t], eta_entry(av[t], i, q, aq), acc);
-                }
-            }
-        }
-        const double v = wave_sum(acc);
-        if (lane == 0) part[s] = v;
-    }
-    tm = tail_mark(P, 1, tm);
-    __syncthreads();
-    const double sy = block_dot_finish(part);
-    tm = tail_mark(P, 2, tm);
-
-    if (tid == 0) {
-        // basis bookkeeping (v4:339-342) + non-basic list swap-remove / append
-        P.c_B[q] = c_p;
-        P.b_ixs[q] = p;
-        if (own_p) {
-            P.nb_list[kp] = last;
-            P.nb_pos[last] = kp;
-            P.nb_pos[p] = -1;
-            --cnt;
-        }
-        if (owns_col(P, leave)) {
-            P.nb_list[cnt] = (int32_t)leave;
-            P.nb_pos[leave] = cnt;
-            ++cnt;
-        }
-        st->nb_count = cnt;
-        // the deferred pivot (spx_device.h)
-        st->aq = aq;
-        st->s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
-        if (y_was_pending) st->y_buf ^= 1;  // k_price of this pass persisted y
-        st->y_applied = it;
-        st->xb_applied = it;
-        st->p = p;
-        st->q = q;
-        st->min_e = min_e;
-        st->iter = it + 1;
-        st_agent(&st->ticket_update, 0u);
-    }
-    tm = tail_mark(P, 3, tm);
+    pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, P.c[p]), min_e, it);
+    st_agent(&st->ticket_update, 0u);
+    tail_mark(P, 1, tm);
 }
 
 template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
-                               const double* a_new, unsigned char* smem);
+                               unsigned char* smem);
 
 template <int BLOCK, int R, bool RS>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
@@ -570,7 +529,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(rrow);
     const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
     const bool upd_x = st->xb_applied < it;
-    const bool y_was_pending = st->y_applied < it;
 
     // s_x = r.b (v4:347) for the deferred x_b update is accumulated inside the
     // row stream (every wave streams all of r; lane-strided, k ascending, then
@@ -656,46 +614,49 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const double s_x = (upd_x && nvalid > 0) ? wave_sum(sxa) : 0.0;
 
     // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
-    // (compute_theta, v4:199-208) and the wave's argmin
-    double wbest = INFINITY;
-    int64_t wi = INT64_MAX;
-    int64_t nonpos = 0;
-    double wT = 0.0;
+    // (compute_theta, v4:199-208) and the wave's ratio-test partial
+    UpdPartial wp = upd_empty();
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         if (u < nvalid) {
             const double a = wave_sum(acc[u]);
             const int64_t i = gr0 + u;
-            if constexpr (RS) wT = fma(P.c_B[i], a, wT);
+            const double cb = P.c_B[i];
             double xb = P.x_b[i];
             if (upd_x) xb = fma(s_x, ei[u], xb);
             if (lane == 0) {
-                st_agent(&a_new[i], a);
+                a_new[i] = a;  // read back by the next pass (own row) / k_flush
                 if (upd_x) P.x_b[i] = xb;
             }
             const bool pos = a > 0.0;
             const double th = pos ? xb / a : INFINITY;
-            nonpos += !pos;
-            if (argmin_better(th, i, wbest, wi)) { wbest = th; wi = i; }
+            wp.nonpos += !pos;
+            wp.T = fma(cb, a, wp.T);
+            if (argmin_better(th, i, wp.theta, wp.idx)) {
+                wp.theta = th;
+                wp.idx = i;
+                wp.a_w = a;
+                wp.cb_w = cb;
+                wp.bix_w = P.b_ixs[i];
+            }
         }
     }
-    drain_vmem();  // every storing wave drains its alpha stores before the barrier
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
-    if (lane == 0) red[wave] = UpdPartial{wbest, wi, nonpos, wT};
+    if (lane == 0) red[wave] = wp;
     __syncthreads();
     if (tid == 0) {
         UpdPartial w = red[0];
-        for (int i = 1; i < WAVES; ++i) {
-            if (argmin_better(red[i].theta, red[i].idx, w.theta, w.idx)) { w.theta = red[i].theta; w.idx = red[i].idx; }
-            w.nonpos += red[i].nonpos;
-            w.T += red[i].T;
-        }
-        st_agent(&P.upd_partials[blockIdx.x].theta, w.theta);
-        st_agent(&P.upd_partials[blockIdx.x].idx, w.idx);
-        st_agent(&P.upd_partials[blockIdx.x].nonpos, w.nonpos);
-        if constexpr (RS) st_agent(&P.upd_partials[blockIdx.x].T, w.T);
-        drain_vmem();
+        for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
+        UpdPartial* dstp = &P.upd_partials[blockIdx.x];
+        st_agent(&dstp->theta, w.theta);
+        st_agent(&dstp->idx, w.idx);
+        st_agent(&dstp->nonpos, w.nonpos);
+        st_agent(&dstp->T, w.T);
+        st_agent(&dstp->a_w, w.a_w);
+        st_agent(&dstp->cb_w, w.cb_w);
+        st_agent(&dstp->bix_w, w.bix_w);
+        drain_vmem();  // the partial is visible before the ticket
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
         *s_last = (t == gridDim.x - 1);
@@ -704,50 +665,23 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
     if constexpr (RS)
-        update_tail_rs<BLOCK>(P, st, it, par, a_prev, a_new, smem);
+        update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem);
     else
-        update_tail<BLOCK>(P, st, p, min_e, it, y_was_pending, a_new, smem);
+        update_tail<BLOCK>(P, st, p, min_e, it, smem);
     stamp_tail(slot, t_tail, win);
 }
 
 // Row-sharded tail (last workgroup of k_update on this rank): the local
-// leaving candidate, the local sum of c_B[i] * alpha_i, and the candidate's
-// row of B^-1_new — recomputed from the old rows exactly as the stream wrote
-// it — into rs_send for the ratio-test all-gather.  No global state changes:
-// k_finalize_rs does them after the exchange.
+// leaving candidate with its scalars, the local sum T of c_B[i] * alpha_i, and
+// the candidate's row of B^-1_new — recomputed from the old rows exactly as the
+// stream wrote it — into rs_send for the ratio-test all-gather.  No global
+// state changes: k_finalize_rs does them after the exchange.
 template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
-                               const double* a_new, unsigned char* smem) {
-    using Lds = UpdLds<BLOCK>;
-    constexpr int WAVES = BLOCK / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
-    // workgroup partials: argmin (total order), nonpos, and T in a fixed order
-    UpdPartial w{INFINITY, INT64_MAX, 0, 0.0};
-    for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
-        const double th = ld_agent(&P.upd_partials[g].theta);
-        const int64_t i = ld_agent(&P.upd_partials[g].idx);
-        w.nonpos += ld_agent(&P.upd_partials[g].nonpos);
-        w.T += ld_agent(&P.upd_partials[g].T);
-        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const double th = __shfl_xor(w.theta, off, 64);
-        const int64_t i = __shfl_xor(w.idx, off, 64);
-        w.nonpos += __shfl_xor(w.nonpos, off, 64);
-        w.T += __shfl_xor(w.T, off, 64);
-        if (argmin_better(th, i, w.theta, w.idx)) { w.theta = th; w.idx = i; }
-    }
-    if (lane == 0) red[wave] = w;
-    __syncthreads();
-    UpdPartial t = red[0];
-#pragma unroll
-    for (int k = 1; k < WAVES; ++k) {
-        if (argmin_better(red[k].theta, red[k].idx, t.theta, t.idx)) { t.theta = red[k].theta; t.idx = red[k].idx; }
-        t.nonpos += red[k].nonpos;
-        t.T += red[k].T;
-    }
+                               unsigned char* smem) {
+    const int tid = threadIdx.x;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
     RsHeader* h = reinterpret_cast<RsHeader*>(P.rs_send);
     double* row = reinterpret_cast<double*>(P.rs_send + sizeof(RsHeader));
     const bool have = t.idx >= P.r0 && t.idx < P.r0 + P.mloc;
@@ -770,9 +704,9 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
         h->idx = have ? t.idx : INT64_MAX;
         h->nonpos = t.nonpos;
         h->T = t.T;
-        h->a_w = have ? ld_agent(&a_new[t.idx]) : 0.0;
-        h->cb_w = have ? P.c_B[t.idx] : 0.0;
-        h->bix_w = have ? P.b_ixs[t.idx] : -1;
+        h->a_w = t.a_w;
+        h->cb_w = t.cb_w;
+        h->bix_w = t.bix_w;
         st_agent(&st->ticket_update, 0u);
     }
 }
@@ -816,38 +750,8 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
     const dbl2* row = reinterpret_cast<const dbl2*>(P.rs_recv + w * P.rs_stride + sizeof(RsHeader));
     dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
     for (int64_t k = tid; k < (P.L >> 1); k += 256) rb[k] = row[k];
-    if (tid == 0) {
-        const double aq = hw->a_w, c_bq = hw->cb_w, c_p = P.c[p];
-        const int64_t leave = hw->bix_w;
-        const double sy = -(T - c_bq * aq) / aq + c_p * (1.0 / aq - 1.0);
-        // basis bookkeeping (v4:339-342) + non-basic list swap-remove / append
-        P.c_B[q] = c_p;
-        P.b_ixs[q] = p;
-        int cnt = st->nb_count;
-        if (owns_col(P, p)) {
-            const int kp = P.nb_pos[p];
-            const int last = P.nb_list[cnt - 1];
-            P.nb_list[kp] = last;
-            P.nb_pos[last] = kp;
-            P.nb_pos[p] = -1;
-            --cnt;
-        }
-        if (owns_col(P, leave)) {
-            P.nb_list[cnt] = (int32_t)leave;
-            P.nb_pos[leave] = cnt;
-            ++cnt;
-        }
-        st->nb_count = cnt;
-        st->aq = aq;
-        st->s_y = sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
-        if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
-        st->y_applied = it;
-        st->xb_applied = it;
-        st->p = p;
-        st->q = q;
-        st->min_e = min_e;
-        st->iter = it + 1;
-    }
+    if (tid == 0)
+        pivot_bookkeeping(P, st, p, q, hw->bix_w, hw->a_w, y_scalar(T, hw->a_w, hw->cb_w, P.c[p]), min_e, it);
 }
 
 // ---------------------------------------------------------------------------

@@ -17,13 +17,14 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
-def test_every_geometry_bit_identical(spx):
-    """Register tail (16 waves, L <= 4096), chunked tail (fewer waves), LDS-y
-    and global-y pricing, every rows-per-wave: the same bits."""
+def test_every_geometry_consistent(spx):
+    """LDS-y and global-y pricing and every pricing block give the same bits;
+    every update geometry (its c_B.alpha sum order) the same pivots and values
+    within 1e-12."""
     m, n, seed, k = 1100, 3300, 4, 150
     runs = []
-    for kw in [dict(), dict(update_block=256), dict(update_block=512, update_rows=2), dict(global_y=True),
-               dict(price_block=256, global_y=True), dict(update_block=1024, update_rows=4)]:
+    for kw in [dict(), dict(global_y=True), dict(price_block=256, global_y=True), dict(price_block=1024),
+               dict(update_block=256), dict(update_block=512, update_rows=2), dict(update_block=1024, update_rows=4)]:
         with spx.Context(m=m, n=n, seed=seed, **kw) as ctx:
             st, piv = ctx.iterate(k)
             s = ctx.state(binv=True)
@@ -33,9 +34,15 @@ def test_every_geometry_bit_identical(spx):
     assert piv0 == k
     for kw, piv, s in runs[1:]:
         assert piv == piv0, kw
-        for key in ("b_ixs", "x_b", "y", "binv"):
-            assert np.array_equal(s[key], s0[key]), (kw, key)
-        assert s["z"] == s0["z"], kw
+        assert np.array_equal(s["b_ixs"], s0["b_ixs"]), kw
+        if any(key.startswith("update_") for key in kw):
+            for key in ("x_b", "y", "binv"):
+                assert _rel(s[key], s0[key]) <= 1e-12, (kw, key)
+            assert abs(s["z"] - s0["z"]) <= 1e-12 * abs(s0["z"]), kw
+        else:
+            for key in ("x_b", "y", "binv"):
+                assert np.array_equal(s[key], s0[key]), (kw, key)
+            assert s["z"] == s0["z"], kw
 
 
 def test_mid_size_against_oracle(spx, oracle):
