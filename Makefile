@@ -52,3 +52,9 @@ pingpong:
 	@mkdir -p $(BUILD)/pp
 	$(HIPCC) $(HIPFLAGS) -DSPX_INPLACE=0 -c $(SRC)/spx_kernels.hip -o $(BUILD)/pp/spx_kernels.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/pp/libsimplex.so $(BUILD)/pp/spx_kernels.o $(BUILD)/spx_api.o $(LDFLAGS)
+
+# diagnostic (timing-only, wrong results): update kernel without its tail
+diag_notail:
+	@mkdir -p $(BUILD)/notail
+	$(HIPCC) $(HIPFLAGS) -DSPX_DIAG_SKIP_TAIL=1 -c $(SRC)/spx_kernels.hip -o $(BUILD)/notail/spx_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/notail/libsimplex.so $(BUILD)/notail/spx_kernels.o $(BUILD)/spx_api.o $(LDFLAGS)

@@ -79,6 +79,8 @@ typedef struct spx_opts {
 #define SPX_FLAG_STAMPS 2 /* in-kernel phase stamps (spx_phase_times); diagnostic */
 #define SPX_FLAG_GLOBAL_Y 4 /* pricing reads y from global memory instead of LDS
                                (automatic when L*8 bytes do not fit in LDS)   */
+#define SPX_FLAG_SPLIT_TAIL 16 /* tuning: run the pivot tail as its own launch
+                                  instead of the update kernel's last workgroup */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass

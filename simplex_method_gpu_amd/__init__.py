@@ -30,6 +30,7 @@ FLAG_TIMING = 1
 FLAG_STAMPS = 2
 FLAG_GLOBAL_Y = 4
 FLAG_ROW_SHARD = 8
+FLAG_SPLIT_TAIL = 16
 
 
 class SolveStatus(IntEnum):
@@ -117,7 +118,7 @@ class Context:
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
-                 global_y: bool = False, row_shard: bool = False):
+                 global_y: bool = False, row_shard: bool = False, split_tail: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -125,7 +126,8 @@ class Context:
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
         o.update_block = update_block
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
-                   | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0))
+                   | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
+                   | (FLAG_SPLIT_TAIL if split_tail else 0))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)

@@ -211,6 +211,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // row shard of B^-1 (SPX_FLAG_ROW_SHARD with nranks > 1): rows
     // [r0, r0 + mloc), ping-pong storage; otherwise all rows, in place
     P.row_shard = (G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD)) ? 1 : 0;
+    P.split_tail = (x->opts.flags & SPX_FLAG_SPLIT_TAIL) ? 1 : 0;
     x->mb = P.row_shard ? (m + G - 1) / G : m;
     P.r0 = P.row_shard ? std::min<int64_t>(m, (int64_t)r * x->mb) : 0;
     P.mloc = P.row_shard ? std::min<int64_t>(m, P.r0 + x->mb) - P.r0 : m;
@@ -354,6 +355,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
+    if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
     if (x->P.row_shard) {  // ratio-test all-gather (header + candidate row), then finalise
         NCCL_TRY(ncclAllGather(x->P.rs_send, x->rs_recv, (size_t)x->P.rs_stride, ncclUint8, x->comm, x->stream));
         HIP_TRY(launch_finalize_rs(x->P, x->stream));
@@ -586,6 +588,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 spx_ctx* x = cs[g];
                 HIP_TRY(hipSetDevice(x->device));
                 HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
+                if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
                 if (rs) HIP_TRY(hipEventRecord(x->ev_sent2, x->stream));
                 else
                     for (int h = 0; h < G; ++h) HIP_TRY(hipStreamWaitEvent(x->stream, cs[h]->ev_recv, 0));
@@ -738,6 +741,7 @@ int spx_pivot(spx_ctx* x, int64_t* q, int32_t* status) {
     if (!x->stepped_price) return fail(SPX_ERR_STATE, "spx_pivot needs a preceding spx_price");
     x->stepped_price = false;
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
+    if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
     SPX_TRY(read_state(x));
     if (q) *q = (x->status == SPX_STATUS_UNBOUNDED) ? -1 : x->st_host->q;
     if (status) *status = x->status;

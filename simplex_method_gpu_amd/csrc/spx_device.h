@@ -128,6 +128,7 @@ struct Params {
     // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
     // global rows [r0, r0 + mloc) of B^-1, stored as B0/B1 (mloc x L ping-pong)
     int32_t row_shard;
+    int32_t split_tail;            // 1: the pivot tail runs as its own launch (k_tail)
     int64_t r0, mloc;
     unsigned char* rs_send;        // RsHeader + row
     const unsigned char* rs_recv;  // nin entries of rs_stride bytes

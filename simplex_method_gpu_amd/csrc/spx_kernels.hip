@@ -365,11 +365,11 @@ __device__ __forceinline__ UpdPartial upd_shfl_xor(const UpdPartial& v, int off)
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
 // order is fixed for a given launch geometry.
 template <int BLOCK>
-__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red) {
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     UpdPartial w = upd_empty();
-    for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
+    for (int g = tid; g < nparts; g += BLOCK) {
         const UpdPartial* src = &P.upd_partials[g];
         UpdPartial v;
         v.theta = ld_agent(&src->theta);
@@ -455,10 +455,10 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
 // vector updates are deferred (spx_device.h).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            unsigned char* smem) {
+                            unsigned char* smem, int nparts) {
     unsigned long long tm = P.stamps ? rtime() : 0;
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
-    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
     tm = tail_mark(P, 0, tm);
     if (threadIdx.x != 0) return;
     const int64_t q = t.idx;
@@ -479,7 +479,7 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
 
 template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
-                               unsigned char* smem);
+                               unsigned char* smem, int nparts);
 
 template <int BLOCK, int R, bool RS>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
@@ -645,6 +645,14 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
     if (lane == 0) red[wave] = wp;
     __syncthreads();
+    if (P.split_tail) {  // k_tail merges after the kernel boundary: plain stores, no fan-in
+        if (tid == 0) {
+            UpdPartial w = red[0];
+            for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
+            P.upd_partials[blockIdx.x] = w;
+        }
+        return;
+    }
     if (tid == 0) {
         UpdPartial w = red[0];
         for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
@@ -664,10 +672,14 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     __syncthreads();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
+#ifdef SPX_DIAG_SKIP_TAIL  // timing-only build: pivots stop after the first pass
+    if (tid == 0) st_agent(&st->ticket_update, 0u);
+    if (true) return;
+#endif
     if constexpr (RS)
-        update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem);
+        update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem, gridDim.x);
     else
-        update_tail<BLOCK>(P, st, p, min_e, it, smem);
+        update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x);
     stamp_tail(slot, t_tail, win);
 }
 
@@ -678,10 +690,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 // state changes: k_finalize_rs does them after the exchange.
 template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
-                               unsigned char* smem) {
+                               unsigned char* smem, int nparts) {
     const int tid = threadIdx.x;
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
-    const UpdPartial t = reduce_update_partials<BLOCK>(P, red);
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
     RsHeader* h = reinterpret_cast<RsHeader*>(P.rs_send);
     double* row = reinterpret_cast<double*>(P.rs_send + sizeof(RsHeader));
     const bool have = t.idx >= P.r0 && t.idx < P.r0 + P.mloc;
@@ -709,6 +721,26 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
         h->bix_w = t.bix_w;
         st_agent(&st->ticket_update, 0u);
     }
+}
+
+// The pivot tail as its own one-workgroup launch (split_tail): the k_update
+// workgroups stored their partials plainly and returned; the kernel boundary
+// makes them visible here.
+__global__ __launch_bounds__(1024) void k_tail(Params P, int nparts) {
+    DevState* st = P.st;
+    if (stopped(st)) return;  // also when k_update found the optimum
+    __shared__ __attribute__((aligned(16))) unsigned char smem[UpdLds<1024>::bytes];
+    double min_e = INFINITY;
+    int64_t p = INT64_MAX;
+    for (int g = 0; g < P.nin; ++g) {
+        const ArgMinEntry e = P.price_in[g];
+        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
+    }
+    const int64_t it = st->iter;
+    if (P.row_shard)
+        update_tail_rs<1024>(P, st, it, (int)(it & 1), (it & 1) ? P.alpha1 : P.alpha0, smem, nparts);
+    else
+        update_tail<1024>(P, st, p, min_e, it, smem, nparts);
 }
 
 // Row-sharded pivot finalisation (one workgroup, after the ratio-test
@@ -990,6 +1022,11 @@ template <int BLOCK, int R>
 static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     return P.row_shard ? launch_update_k<BLOCK, R, true>(P, grid, s, e0, e1)
                        : launch_update_k<BLOCK, R, false>(P, grid, s, e0, e1);
+}
+
+hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
+    hipLaunchKernelGGL(k_tail, dim3(1), dim3(1024), 0, s, P, nparts);
+    return hipGetLastError();
 }
 
 hipError_t launch_finalize_rs(const Params& P, hipStream_t s) {

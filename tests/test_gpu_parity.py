@@ -117,7 +117,7 @@ def test_graph_eager_and_tunings_bit_identical(spx):
     m, n, seed, k = 300, 1200, 7, 120
     runs = []
     variants = [dict(), dict(graph_batch=-1), dict(graph_batch=5), dict(price_block=1024), dict(price_grid=3),
-                dict(update_rows=4), dict(update_rows=8), dict(update_block=256)]
+                dict(split_tail=True), dict(update_rows=4), dict(update_rows=8), dict(update_block=256)]
     for kw in variants:
         with spx.Context(m=m, n=n, seed=seed, **kw) as ctx:
             ctx.iterate(k)
