@@ -261,14 +261,25 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     int64_t want = (x->max_local_cols + waves - 1) / waves;
     int64_t cap = (int64_t)x->cus * per_cu;
     pc.grid = (int)std::max<int64_t>(1, std::min(want, cap));
+    // small problems (C2): under 2 columns per wave the per-workgroup y staging
+    // and fan-in dominate — one workgroup per CU (measured 13.0 -> 10.4 us)
+    if (x->max_local_cols < 2LL * pc.grid * waves)
+        pc.grid = (int)std::max<int64_t>(1, std::min<int64_t>(pc.grid, std::max<int64_t>(x->cus,
+                                                                   x->max_local_cols / (2 * waves))));
     if (x->opts.price_grid > 0) pc.grid = x->opts.price_grid;
 
     UpdateCfg& uc = x->ucfg;
     int ub = x->opts.update_block;
     // measured (tools/itbench.py): 16 waves x 1 row at m <= 8192 (C3: 1024x1),
     // 8 waves x 2 rows beyond (C5: 512x2, 4.3 GB streamed per launch)
-    const bool big_m = m > 8192;
-    if (!(ub == 256 || ub == 512 || ub == 1024)) ub = big_m ? 512 : 1024;
+    // and for small m the largest block that still gives every CU a workgroup
+    // (C2, m=1024: 256 threads, update 20 -> 14 us)
+    const int64_t rows_here = P.mloc;
+    const bool big_m = rows_here > 8192;
+    if (!(ub == 256 || ub == 512 || ub == 1024)) {
+        ub = big_m ? 512 : 1024;
+        while (ub > 256 && rows_here / (ub / 64) < x->cus) ub /= 2;
+    }
     int rows = x->opts.update_rows;
     if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = big_m ? 2 : 1;
     if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
