@@ -26,8 +26,8 @@ $(BUILD)/spx_api.o: $(SRC)/spx_api.cpp $(SRC)/spx_kernels.h $(SRC)/spx_device.h 
 $(LIB): $(BUILD)/spx_kernels.o $(BUILD)/spx_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDFLAGS)
 
-$(CLI): $(SRC)/solver_main.cpp include/simplex.h $(LIB)
-	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG) -Wl,-rpath,'$$ORIGIN/$(PKG)' -lsimplex
+$(CLI): $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp $(SRC)/lp_io.h include/simplex.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -pthread -Iinclude -o $@ $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp -L$(PKG) -Wl,-rpath,'$$ORIGIN/$(PKG)' -lsimplex
 
 oracle:
 	$(MAKE) -C oracle

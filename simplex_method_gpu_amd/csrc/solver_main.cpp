@@ -14,6 +14,11 @@
 //   --device D     HIP device ordinal
 //   --no-iter-lines  suppress the "# Iteration k" lines
 //   --json         also print one JSON result line
+//   --threads T    text-parser threads (default: min(16, cores))
+//   --write-bin F  write the loaded/generated LP as binary .spxlp (lp_io.h)
+//   --write-text F write it in the reference's text format (%.17g, exact)
+//   --no-solve     stop after reading/writing
+// The input file may be text or binary; binary is detected by its magic.
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
@@ -26,6 +31,7 @@
 #include <vector>
 
 #include "../../include/simplex.h"
+#include "lp_io.h"
 
 using Clock = std::chrono::steady_clock;
 using TimePoint = Clock::time_point;
@@ -39,20 +45,9 @@ static void print_elapsed_time(const char* msg, double dur) {
     std::cout << std::setw(6) << dur << '\n';
 }
 
-static bool load_matrix(std::ifstream& file, double* a, int64_t m, int64_t n, const char* name) {
-    // row-major text -> column-major storage (R2C, v4:59-60,94-104)
-    for (int64_t i = 0; i < m; ++i)
-        for (int64_t j = 0; j < n; ++j)
-            if (!(file >> a[i + j * m])) {
-                std::cerr << "Failed to read (" << i << "," << j << ") for " << name << "\n";
-                return false;
-            }
-    return true;
-}
-
 static void usage() {
     std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
-                 " (<file> | --gen m n seed)\n";
+                 " [--threads T] [--write-bin F] [--write-text F] [--no-solve] (<file> | --gen m n seed)\n";
 }
 
 int main(int argc, char* argv[]) {
@@ -60,7 +55,9 @@ int main(int argc, char* argv[]) {
     int64_t max_iter = INT64_MAX;
     double eps = 1e-7;
     int device = -1;
-    bool iter_lines = true, json = false, gen = false;
+    bool iter_lines = true, json = false, gen = false, solve = true;
+    int threads = 0;
+    std::string write_bin, write_text;
     int64_t gm = 0, gn = 0;
     uint64_t gseed = 0;
     const char* path = nullptr;
@@ -78,6 +75,10 @@ int main(int argc, char* argv[]) {
         else if (s == "--device") { need(1); device = std::atoi(argv[++a]); }
         else if (s == "--no-iter-lines") iter_lines = false;
         else if (s == "--json") json = true;
+        else if (s == "--threads") { need(1); threads = std::atoi(argv[++a]); }
+        else if (s == "--write-bin") { need(1); write_bin = argv[++a]; }
+        else if (s == "--write-text") { need(1); write_text = argv[++a]; }
+        else if (s == "--no-solve") solve = false;
         else if (s == "--gen") {
             need(3);
             gen = true;
@@ -95,31 +96,28 @@ int main(int argc, char* argv[]) {
 
     const TimePoint t_start = Clock::now();
     TimePoint t_host_alloc = t_start, t_read = t_start, t_solve = t_start;
-    int64_t m = 0, n = 0;
-    std::vector<double> A, b, c;
+    lpio::LP lp;
+    std::string err;
     if (!gen) {
-        std::ifstream file(path);
-        if (!file.is_open()) {
-            std::cerr << "Could not open " << path << ".\n";
-            return 1;
-        }
-        if (!(file >> m >> n) || m > n) {
-            std::cerr << "Either failed to read m and n, or m > n.\n";
-            return 1;
-        }
-        t_host_alloc = Clock::now();
-        A.resize((size_t)(m * n));
-        b.resize((size_t)m);
-        c.resize((size_t)n);
-        t_read = Clock::now();
-        if (!load_matrix(file, A.data(), m, n, "A") || !load_matrix(file, b.data(), m, 1, "b") ||
-            !load_matrix(file, c.data(), 1, n, "c"))
-            return EXIT_FAILURE;
-    } else {
-        m = gm;
-        n = gn;
         t_host_alloc = t_read = Clock::now();
+        if (lpio::read_any(path, lp, err, threads) != 0) {
+            std::cerr << err << "\n";
+            return EXIT_FAILURE;
+        }
+    } else {
+        lp.m = gm;
+        lp.n = gn;
+        t_host_alloc = t_read = Clock::now();
+        if (!write_bin.empty() || !write_text.empty()) lpio::generate(gm, gn, gseed, lp);
     }
+    if ((!write_bin.empty() && lpio::write_binary(write_bin, lp, err) != 0) ||
+        (!write_text.empty() && lpio::write_text(write_text, lp, err) != 0)) {
+        std::cerr << err << "\n";
+        return EXIT_FAILURE;
+    }
+    if (!solve) return 0;
+    const int64_t m = lp.m, n = lp.n;
+    const bool device_gen = gen && lp.A.empty();
     std::vector<double> x_b((size_t)std::max<int64_t>(m, 1));
     std::vector<int64_t> b_ixs((size_t)std::max<int64_t>(m, 1));
 
@@ -130,8 +128,8 @@ int main(int argc, char* argv[]) {
     o.device = device;
     spx_ctx* ctx = nullptr;
     const TimePoint t_alloc = Clock::now();
-    int rc = gen ? spx_create_generated(&ctx, m, n, gseed, &o)
-                 : spx_create(&ctx, m, n, A.data(), b.data(), c.data(), &o);
+    int rc = device_gen ? spx_create_generated(&ctx, m, n, gseed, &o)
+                        : spx_create(&ctx, m, n, lp.A.data(), lp.b.data(), lp.c.data(), &o);
     if (rc != SPX_OK) {
         std::cerr << "spx_create failed (" << rc << "): " << spx_last_error() << "\n";
         return EXIT_FAILURE;
@@ -167,8 +165,7 @@ int main(int argc, char* argv[]) {
     }
     std::cout << '\n';
     const TimePoint t_host_free = Clock::now();
-    A.clear();
-    A.shrink_to_fit();
+    lp = lpio::LP();
     const TimePoint t_end = Clock::now();
 
     // timing table (v4:456-471).  The reference's y / x_b phases are fused into

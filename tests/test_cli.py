@@ -59,3 +59,86 @@ def test_generated_solve_json():
 
     js = json.loads(r.stdout.strip().splitlines()[-1])
     assert js["status"] == 1 and abs(js["z"] - 115.9505237149796) < 1e-9 * 116
+
+
+# --- LP file formats (simplex_method_gpu_amd/csrc/lp_io.h) ---
+
+def _numbers(path):
+    return [float(t) for t in open(path).read().split()]
+
+
+def test_bad_token_messages(tmp_path):
+    """Parallel parser reports the first unreadable entry like the reference's
+    sequential reader (v4:94-104): A by (i,j), b by (i,0), c by (0,j)."""
+    for text, msg in [("2 3\n1 2 3\n4 x 6\n1 1\n1 1 1\n", "Failed to read (1,1) for A"),
+                      ("2 3\n1 2 3\n4 5 6\n7 8\n", "Failed to read (0,0) for c"),
+                      ("2 3\n1 2 3\n4 5 6\n7\n", "Failed to read (1,0) for b"),
+                      ("2 3\n1 2 3\n4 5 6\n7 8\n1 2 z\n", "Failed to read (0,2) for c"),
+                      ("two 3\n", "Either failed to read m and n, or m > n.")]:
+        p = tmp_path / "lp.txt"
+        p.write_text(text)
+        r = run("--no-solve", str(p))
+        assert r.returncode == 1 and r.stderr == msg + "\n", (text, r.stderr)
+
+
+def test_text_binary_round_trip(tmp_path):
+    """text -> .spxlp -> text keeps every number (%.17g) and ignores trailing prose."""
+    src = tmp_path / "src.txt"
+    src.write_text(open(SAMPLE).read() + "\nthis trailing comment is ignored 1 2 3\n")
+    b1, t1 = tmp_path / "a.spxlp", tmp_path / "a.txt"
+    assert run("--no-solve", "--write-bin", str(b1), str(src)).returncode == 0
+    assert open(b1, "rb").read(8) == b"SPXLP001"
+    assert run("--no-solve", "--write-text", str(t1), str(b1)).returncode == 0
+    want = _numbers(SAMPLE)
+    assert _numbers(t1) == want[:2 + 2 * 4 + 2 + 4]
+
+
+def test_generated_export_matches_oracle(tmp_path, oracle):
+    """--gen ... --write-text exports the seeded LP bit for bit (host copy of k_generate)."""
+    import numpy as np
+
+    m, n, seed = 37, 150, 5
+    t = tmp_path / "g.txt"
+    assert run("--no-solve", "--write-text", str(t), "--gen", str(m), str(n), str(seed)).returncode == 0
+    v = np.array(_numbers(t))
+    A, b, c = oracle.generate(m, n, seed)
+    assert v[:2].tolist() == [m, n]
+    assert np.array_equal(v[2:2 + m * n].reshape(m, n), A.T)
+    assert np.array_equal(v[2 + m * n:2 + m * n + m], b) and np.array_equal(v[2 + m * n + m:], c)
+
+
+def test_parallel_parse_matches_single_thread(tmp_path):
+    """A multi-MiB file parsed by 1 and by 7 threads gives the same binary."""
+    t = tmp_path / "big.txt"
+    assert run("--no-solve", "--write-text", str(t), "--gen", "300", "2000", "9").returncode == 0
+    assert os.path.getsize(t) > 8 << 20
+    outs = []
+    for th in ("1", "7"):
+        o = tmp_path / f"big{th}.spxlp"
+        assert run("--no-solve", "--threads", th, "--write-bin", str(o), str(t)).returncode == 0
+        outs.append(open(o, "rb").read())
+    assert outs[0] == outs[1] and len(outs[0]) == 24 + 8 * (300 * 2000 + 300 + 2000)
+
+
+def test_truncated_binary(tmp_path):
+    b1 = tmp_path / "a.spxlp"
+    assert run("--no-solve", "--write-bin", str(b1), SAMPLE).returncode == 0
+    data = open(b1, "rb").read()
+    (tmp_path / "cut.spxlp").write_bytes(data[:-8])
+    r = run("--no-solve", str(tmp_path / "cut.spxlp"))
+    assert r.returncode == 1 and "truncated" in r.stderr
+
+
+@pytest.mark.gpu
+def test_binary_solve_matches_text(tmp_path):
+    """Solving the .spxlp export gives the same stdout result block as the text file."""
+    t, b1 = tmp_path / "g.txt", tmp_path / "g.spxlp"
+    assert run("--no-solve", "--write-text", str(t), "--write-bin", str(b1), "--gen", "64", "256", "0").returncode == 0
+    outs = []
+    for f in (t, b1, None):
+        args = ["--no-iter-lines", "--json"] + ([str(f)] if f else ["--gen", "64", "256", "0"])
+        r = run(*args)
+        assert r.returncode == 0, r.stderr
+        lines = r.stdout.splitlines()
+        outs.append(lines[:lines.index("")])
+    assert outs[0] == outs[1] == outs[2] and outs[0][0].startswith("Optimum found: ")
