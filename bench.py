@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--update-block", type=int, default=0)
     ap.add_argument("--price-block", type=int, default=0)
     ap.add_argument("--graph-batch", type=int, default=0)
+    ap.add_argument("--window", type=int, default=0,
+                    help="B^-1 representation: 0 library default, -1 explicit rank-1 update, 8/16/32/64 eta window")
     ap.add_argument("--replicated", action="store_true",
                     help="N > 1: keep B^-1 replicated instead of row-sharded (SPX_FLAG_ROW_SHARD)")
     a = ap.parse_args()
@@ -87,7 +89,7 @@ def main():
         ctx = spx.Context(m=m, n=n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
                           update_rows=args.update_rows, update_block=args.update_block,
                           price_block=args.price_block, graph_batch=args.graph_batch,
-                          row_shard=(world > 1 and not args.replicated))
+                          row_shard=(world > 1 and not args.replicated), window=args.window)
         if world > 1:
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 1
+#define SPX_ABI_VERSION 2
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -72,7 +72,13 @@ typedef struct spx_opts {
     int32_t price_grid;   /* tuning: pricing workgroups, 0 = auto              */
     int32_t flags;        /* SPX_FLAG_* bits                                   */
     int32_t update_block; /* tuning: threads per update workgroup, 0 = auto    */
-    int32_t reserved[5];
+    int32_t window;       /* B^-1 representation: 0 = auto,
+                             -1 = explicit B^-1 rewritten by a rank-1 update
+                             every pivot (v4:331-333), 8/16/32/64 = eta window:
+                             B^-1 = B_w + U R kept for up to window-1 pivots,
+                             then folded by one rank-(window-1) update.  The
+                             window is single-shard / replicated-B^-1 only.   */
+    int32_t reserved[4];
 } spx_opts;
 
 #define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times)  */

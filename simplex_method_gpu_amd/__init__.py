@@ -118,13 +118,14 @@ class Context:
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
-                 global_y: bool = False, row_shard: bool = False, split_tail: bool = False):
+                 global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
         o.eps, o.device, o.rank, o.nranks = eps, device, rank, nranks
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
         o.update_block = update_block
+        o.window = window  # 0 auto, -1 explicit rank-1 B^-1 update, 8/16/32/64 eta window
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
                    | (FLAG_SPLIT_TAIL if split_tail else 0))

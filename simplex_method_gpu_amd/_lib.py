@@ -30,7 +30,8 @@ class SpxOpts(ctypes.Structure):
         ("price_grid", ctypes.c_int32),
         ("flags", ctypes.c_int32),
         ("update_block", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 5),
+        ("window", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 4),
     ]
 
 

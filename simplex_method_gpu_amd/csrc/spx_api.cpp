@@ -120,6 +120,7 @@ struct spx_ctx {
     int64_t pivots = 0;
     int32_t status = SPX_STATUS_MAX_ITER;
     bool stepped_price = false;
+    int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
 
     template <typename T>
     int alloc(T** p, size_t count) {
@@ -236,6 +237,23 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
     SPX_TRY(x->alloc(&P.st, 1));
 
+    // B^-1 representation: eta window of KW pivots, or the explicit rank-1 update
+    int KW = x->opts.window;
+    if (KW == 0) KW = -1;  // auto: explicit B^-1
+    if (KW > 0 && P.row_shard) return fail(SPX_ERR_ARG, "the eta window needs replicated B^-1 (no row sharding)");
+    if (KW > 0 && !(KW == 8 || KW == 16 || KW == 32 || KW == 64))
+        return fail(SPX_ERR_ARG, "window must be 8, 16, 32 or 64 (got %d)", KW);
+    if (KW < -1) return fail(SPX_ERR_ARG, "bad window %d", KW);
+    P.win = KW > 0 ? KW : 0;
+    if (P.win) {
+        SPX_TRY(x->alloc(&P.U, (size_t)(m * KW)));
+        SPX_TRY(x->alloc(&P.Wt, (size_t)((n + 1) * KW)));
+        SPX_TRY(x->alloc(&P.Qrows, (size_t)(KW * L)));
+        SPX_TRY(x->alloc(&P.Urows, (size_t)(KW * KW)));
+        SPX_TRY(x->alloc(&P.SY, (size_t)KW));
+    }
+    P.pr_stride = P.win ? 1 + P.win / 2 : 1;
+
     // column shard: structural and slack columns each split in G contiguous blocks
     int64_t rng[4];
     shard_range(m, n, r, G, rng);
@@ -252,8 +270,12 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         pc.block = x->opts.price_block;
     else
         pc.block = ybytes <= 72 * 1024 ? 512 : 1024;
-    pc.lds_y = ybytes + (size_t)pc.block * 16 + 16 <= 150 * 1024 && !(x->opts.flags & SPX_FLAG_GLOBAL_Y);
-    pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (size_t)pc.block * sizeof(ArgMinEntry) + 16;
+    const size_t red_bytes = (size_t)(pc.block / 64) * sizeof(PricePartial) + 16;
+    const size_t lds_cap = 150 * 1024;
+    pc.lds_y = ybytes + red_bytes <= lds_cap && !(x->opts.flags & SPX_FLAG_GLOBAL_Y);
+    // eta window: the pending base row next to y when both fit
+    pc.wm = !P.win ? 0 : ((pc.lds_y && 2 * ybytes + red_bytes <= lds_cap) ? 1 : 2);
+    pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (pc.wm == 1 ? ybytes : 0) + red_bytes;
     int per_cu = 0;
     HIP_TRY(price_prepare(pc, &per_cu));
     if (per_cu < 1) per_cu = 1;
@@ -294,8 +316,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         SPX_TRY(x->alloc(&P.stamps, 32));
         SPX_TRY(reset_stamps(x));
     }
-    SPX_TRY(x->alloc(&x->send, 1));
-    SPX_TRY(x->alloc(&x->recv, (size_t)G));
+    SPX_TRY(x->alloc(&x->send, (size_t)P.pr_stride));
+    SPX_TRY(x->alloc(&x->recv, (size_t)(G * P.pr_stride)));
     if (P.row_shard) {
         P.rs_stride = (int64_t)sizeof(RsHeader) + 8 * L;
         unsigned char *sb = nullptr, *rb = nullptr;
@@ -312,6 +334,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     int gb = x->opts.graph_batch;
     if (gb == 0) gb = (G > 1) ? -1 : 16;  // RCCL passes are launched eagerly unless asked
     x->batch = (gb < 0 || x->timing) ? 0 : gb;
+    // eta window: a captured batch starts with a fold and spans whole windows
+    if (x->batch > 0 && P.win) x->batch = (int)round_up(x->batch, P.win - 1);
     return SPX_OK;
 }
 
@@ -326,7 +350,17 @@ int do_reset(spx_ctx* x) {
     x->pivots = 0;
     x->status = SPX_STATUS_MAX_ITER;
     x->stepped_price = false;
+    x->nw = 0;
     return SPX_OK;
+}
+
+// Eta window: a fold is due before a pass that starts with nw == KW; each
+// pass adds one pivot (a pass that makes none leaves the device's nw behind
+// the host's count — harmless: k_fold re-checks nw, and every call starts
+// from a readback).
+bool fold_due(const spx_ctx* x) { return x->P.win && x->nw >= x->P.win; }
+void advance_window(spx_ctx* x, bool folded) {
+    if (x->P.win) x->nw = (folded ? 1 : x->nw) + 1;
 }
 
 // One loop pass: pricing, (MINLOC exchange), fused update.
@@ -359,10 +393,14 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         ++x->n_price;
         ++x->n_update;
     }
+    const bool fold = fold_due(x);
+    if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+    advance_window(x, fold);
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, p0, p1));
     if (x->opts.nranks > 1) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
-        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry), ncclUint8, x->comm, x->stream));
+        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
+                               x->stream));
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
@@ -378,13 +416,20 @@ int build_graph(spx_ctx* x) {
     if (x->graph_exec || x->batch <= 0) return SPX_OK;
     HIP_TRY(hipStreamBeginCapture(x->stream, hipStreamCaptureModeThreadLocal));
     int rc = SPX_OK;
+    const int nw_keep = x->nw;
+    if (x->P.win) x->nw = x->P.win;  // a batch starts with a fold (see iterate)
     for (int i = 0; i < x->batch && rc == SPX_OK; ++i) rc = enqueue_pass(x, false);
+    x->nw = nw_keep;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(x->stream, &g);
     if (rc != SPX_OK) return rc;
     if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
     x->graph = g;
     HIP_TRY(hipGraphInstantiate(&x->graph_exec, g, nullptr, nullptr, 0));
+    // the first launch of a fresh graph pays its upload (measured 13 ms for a
+    // 63-node graph): do it here, not inside somebody's timed loop
+    HIP_TRY(hipGraphUpload(x->graph_exec, x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
     return SPX_OK;
 }
 
@@ -393,6 +438,8 @@ int read_state(spx_ctx* x) {
     HIP_TRY(hipStreamSynchronize(x->stream));
     x->pivots = x->st_host->iter;
     x->status = x->st_host->status;  // ST_RUNNING == SPX_STATUS_MAX_ITER
+    x->nw = x->st_host->nw;
+    if (x->status == ST_WINDOW_FULL) return fail(SPX_ERR_STATE, "internal error: eta window overflow");
     return SPX_OK;
 }
 
@@ -400,6 +447,10 @@ int read_state(spx_ctx* x) {
 // vectors in HBM are current.  Not valid between spx_price and spx_pivot.
 int flush(spx_ctx* x) {
     if (x->stepped_price) return fail(SPX_ERR_STATE, "state readback between spx_price and spx_pivot");
+    if (x->P.win) {  // fold every complete pivot: the explicit form the readback kernels expect
+        HIP_TRY(launch_fold(x->P, 2, x->cus, x->stream));
+        x->nw = std::min(x->nw, 1);
+    }
     HIP_TRY(launch_flush(x->P, x->stream));
     return SPX_OK;
 }
@@ -429,20 +480,28 @@ int iterate(spx_ctx* x, int64_t k) {
     if (x->status != SPX_STATUS_MAX_ITER || k <= 0) return SPX_OK;
     if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
     SPX_TRY(set_limit(x, x->pivots + k));
-    // exactly k passes: whole captured batches, then the remainder eagerly
-    int64_t eager = k;
-    if (x->batch > 0 && k >= x->batch) {
-        SPX_TRY(build_graph(x));
-        const int64_t reps = k / x->batch;
-        for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
-        eager = k - reps * x->batch;
+    // exactly k passes: whole captured batches, then the remainder eagerly.
+    // Eta window: batches are captured starting with a fold, so eager passes
+    // first bring the window to nw == KW.
+    int64_t left = k;
+    if (x->batch > 0) {
+        const int64_t lead = x->P.win ? std::max(0, x->P.win - x->nw) : 0;
+        if (left >= lead + x->batch) {
+            for (int64_t i = 0; i < lead; ++i) SPX_TRY(enqueue_pass(x, x->timing));
+            left -= lead;
+            SPX_TRY(build_graph(x));
+            const int64_t reps = left / x->batch;
+            for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
+            left -= reps * x->batch;  // a batch of whole windows leaves nw == KW again
+        }
     }
-    for (int64_t i = 0; i < eager; ++i) SPX_TRY(enqueue_pass(x, x->timing));
+    for (int64_t i = 0; i < left; ++i) SPX_TRY(enqueue_pass(x, x->timing));
     return read_state(x);
 }
 
 int create_tail(spx_ctx* x) {
     SPX_TRY(do_reset(x));
+    if (x->opts.nranks == 1) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
     return SPX_OK;
 }
 
@@ -461,10 +520,12 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
     spx_ctx* x = new spx_ctx();
     int rc = setup_common(x, m, n, opts);
     if (rc == SPX_OK) {
-        hipError_t e = hipMemcpy2DAsync(x->A, (size_t)x->L * 8, A, (size_t)m * 8, (size_t)m * 8, (size_t)n,
-                                        hipMemcpyHostToDevice, x->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(x->b, b, (size_t)m * 8, hipMemcpyHostToDevice, x->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice, x->stream);
+        // blocking copies from pageable memory, after the zero-fills queued on the stream
+        hipError_t e = hipStreamSynchronize(x->stream);
+        if (e == hipSuccess)
+            e = hipMemcpy2D(x->A, (size_t)x->L * 8, A, (size_t)m * 8, (size_t)m * 8, (size_t)n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(x->b, b, (size_t)m * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     }
     if (rc == SPX_OK) rc = create_tail(x);
@@ -563,7 +624,8 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
         if (x->comm_ready) return fail(SPX_ERR_STATE, "group contexts must not have a communicator");
         if (x->m != cs[0]->m || x->n != cs[0]->n) return fail(SPX_ERR_ARG, "group shape mismatch");
         if (x->status != cs[0]->status || x->pivots != cs[0]->pivots) return fail(SPX_ERR_STATE, "group out of step");
-        if (x->P.row_shard != cs[0]->P.row_shard) return fail(SPX_ERR_ARG, "group mixes storage modes");
+        if (x->P.row_shard != cs[0]->P.row_shard || x->P.win != cs[0]->P.win)
+            return fail(SPX_ERR_ARG, "group mixes storage modes");
         if (!x->ev_sent) {
             HIP_TRY(hipSetDevice(x->device));
             HIP_TRY(hipEventCreateWithFlags(&x->ev_sent, hipEventDisableTiming));
@@ -581,16 +643,20 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
             for (int g = 0; g < G; ++g) {  // pricing on every shard
                 spx_ctx* x = cs[g];
                 HIP_TRY(hipSetDevice(x->device));
+                const bool fold = fold_due(x);
+                if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+                advance_window(x, fold);
                 HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
                 HIP_TRY(hipEventRecord(x->ev_sent, x->stream));
             }
-            for (int h = 0; h < G; ++h) {  // all-gather of the 16-byte candidates
+            for (int h = 0; h < G; ++h) {  // all-gather of the candidate records
                 spx_ctx* x = cs[h];
                 HIP_TRY(hipSetDevice(x->device));
+                const int ps = x->P.pr_stride;
                 for (int g = 0; g < G; ++g) {
                     HIP_TRY(hipStreamWaitEvent(x->stream, cs[g]->ev_sent, 0));
-                    HIP_TRY(hipMemcpyAsync(x->recv + g, cs[g]->send, sizeof(ArgMinEntry), hipMemcpyDefault,
-                                           x->stream));
+                    HIP_TRY(hipMemcpyAsync(x->recv + g * ps, cs[g]->send, sizeof(ArgMinEntry) * ps,
+                                           hipMemcpyDefault, x->stream));
                 }
                 HIP_TRY(hipEventRecord(x->ev_recv, x->stream));
             }
@@ -674,24 +740,34 @@ int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_
     const size_t mb = (size_t)x->m * 8;
     SPX_TRY(flush(x));
     SPX_TRY(gather_xb(x));
-    SPX_TRY(read_state(x));  // y_buf after the flush
-    if (x_b) HIP_TRY(hipMemcpyAsync(x_b, x->P.x_b, mb, hipMemcpyDeviceToHost, x->stream));
-    if (b_ixs) HIP_TRY(hipMemcpyAsync(b_ixs, x->P.b_ixs, mb, hipMemcpyDeviceToHost, x->stream));
-    if (y) HIP_TRY(hipMemcpyAsync(y, x->st_host->y_buf ? x->P.y1 : x->P.y0, mb, hipMemcpyDeviceToHost, x->stream));
-    if (c_b) HIP_TRY(hipMemcpyAsync(c_b, x->P.c_B, mb, hipMemcpyDeviceToHost, x->stream));
+    // Device work is enqueued and drained first; the copies into (pageable)
+    // caller memory are then plain blocking copies: an async 2D D2H copy into
+    // pageable memory was seen to overtake the materialising kernel.
+    double* tmp = nullptr;
     if (binv) {
-        double* tmp = nullptr;
         const size_t rows = (size_t)std::max<int64_t>(x->m, (int64_t)x->opts.nranks * x->mb);
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), rows * x->L * 8, x->stream));
-        if (x->P.row_shard) HIP_TRY(hipMemsetAsync(tmp, 0, rows * x->L * 8, x->stream));
-        HIP_TRY(launch_materialize(x->P, tmp, x->stream));
-        if (x->P.row_shard && x->comm_ready)
-            NCCL_TRY(ncclAllGather(tmp + x->P.r0 * x->L, tmp, (size_t)(x->mb * x->L), ncclFloat64, x->comm,
-                                   x->stream));
-        HIP_TRY(hipMemcpy2DAsync(binv, mb, tmp, (size_t)x->L * 8, mb, (size_t)x->m, hipMemcpyDeviceToHost, x->stream));
-        HIP_TRY(hipFreeAsync(tmp, x->stream));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&tmp), rows * x->L * 8));
+        int rc = SPX_OK;
+        hipError_t e = hipSuccess;
+        if (x->P.row_shard) e = hipMemsetAsync(tmp, 0, rows * x->L * 8, x->stream);
+        if (e == hipSuccess) e = launch_materialize(x->P, tmp, x->stream);
+        if (e == hipSuccess && x->P.row_shard && x->comm_ready) {
+            const ncclResult_t r = ncclAllGather(tmp + x->P.r0 * x->L, tmp, (size_t)(x->mb * x->L), ncclFloat64,
+                                                 x->comm, x->stream);
+            if (r != ncclSuccess) rc = fail(SPX_ERR_RCCL, "binv all-gather: %s", ncclGetErrorString(r));
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
+        if (e == hipSuccess && rc == SPX_OK)
+            e = hipMemcpy2D(binv, mb, tmp, (size_t)x->L * 8, mb, (size_t)x->m, hipMemcpyDeviceToHost);
+        (void)hipFree(tmp);
+        if (rc != SPX_OK) return rc;
+        if (e != hipSuccess) return fail(SPX_ERR_HIP, "binv readback: %s", hipGetErrorString(e));
     }
-    SPX_TRY(read_state(x));
+    SPX_TRY(read_state(x));  // drains the stream; y_buf after the flush
+    if (x_b) HIP_TRY(hipMemcpy(x_b, x->P.x_b, mb, hipMemcpyDeviceToHost));
+    if (b_ixs) HIP_TRY(hipMemcpy(b_ixs, x->P.b_ixs, mb, hipMemcpyDeviceToHost));
+    if (y) HIP_TRY(hipMemcpy(y, x->st_host->y_buf ? x->P.y1 : x->P.y0, mb, hipMemcpyDeviceToHost));
+    if (c_b) HIP_TRY(hipMemcpy(c_b, x->P.c_B, mb, hipMemcpyDeviceToHost));
     if (status) *status = x->status;
     if (pivots) *pivots = x->pivots;
     return SPX_OK;
@@ -701,11 +777,12 @@ int spx_reduced_costs(spx_ctx* x, double* e) {
     if (!x || !e) return fail(SPX_ERR_ARG, "NULL argument");
     SPX_TRY(flush(x));
     double* tmp = nullptr;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tmp), (size_t)x->n * 8, x->stream));
-    HIP_TRY(launch_reduced_costs(x->P, tmp, x->stream));
-    HIP_TRY(hipMemcpyAsync(e, tmp, (size_t)x->n * 8, hipMemcpyDeviceToHost, x->stream));
-    HIP_TRY(hipFreeAsync(tmp, x->stream));
-    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&tmp), (size_t)x->n * 8));
+    hipError_t er = launch_reduced_costs(x->P, tmp, x->stream);
+    if (er == hipSuccess) er = hipStreamSynchronize(x->stream);
+    if (er == hipSuccess) er = hipMemcpy(e, tmp, (size_t)x->n * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(tmp);
+    if (er != hipSuccess) return fail(SPX_ERR_HIP, "reduced costs: %s", hipGetErrorString(er));
     return SPX_OK;
 }
 
@@ -728,18 +805,22 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     if (x->status != SPX_STATUS_MAX_ITER) return fail(SPX_ERR_STATE, "solve already terminated");
     SPX_TRY(set_limit(x, x->pivots + 1));
+    const bool fold = fold_due(x);
+    if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
+    const int ps = x->P.pr_stride;
     if (x->opts.nranks > 1) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
-        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry), ncclUint8, x->comm, x->stream));
+        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * ps, ncclUint8, x->comm, x->stream));
     }
-    std::vector<ArgMinEntry> cand((size_t)x->opts.nranks);
-    HIP_TRY(hipMemcpyAsync(cand.data(), x->P.price_in, sizeof(ArgMinEntry) * cand.size(), hipMemcpyDeviceToHost,
-                           x->stream));
+    std::vector<ArgMinEntry> cand((size_t)x->opts.nranks * ps);
     HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(cand.data(), x->P.price_in, sizeof(ArgMinEntry) * cand.size(), hipMemcpyDeviceToHost));
     ArgMinEntry best{INFINITY, INT64_MAX};
-    for (const ArgMinEntry& e : cand)
+    for (int g = 0; g < x->opts.nranks; ++g) {
+        const ArgMinEntry& e = cand[(size_t)g * ps];
         if (argmin_better(e.val, e.idx, best.val, best.idx)) best = e;
+    }
     if (p) *p = (best.idx == INT64_MAX) ? -1 : best.idx;
     if (min_e) *min_e = best.val;
     if (optimal) *optimal = (best.val >= -x->opts.eps || best.idx == INT64_MAX) ? 1 : 0;
@@ -831,7 +912,10 @@ int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb,
     if (ld) *ld = x->L;
     if (local_nb) *local_nb = x->st_host->nb_count;
     if (bp) *bp = 8.0 * (double)(x->m + 1) * (double)x->st_host->nb_count;
-    if (bu) *bu = 16.0 * (double)x->m * (double)x->m;
+    // update bytes per pivot: B^-1 read + write, or (eta window) B_w read plus
+    // the fold's read + write spread over its KW-1 pivots
+    if (bu) *bu = x->P.win ? 8.0 * (double)x->m * (double)x->m * (1.0 + 2.0 / (x->P.win - 1))
+                           : 16.0 * (double)x->m * (double)x->m;
     return SPX_OK;
 }
 

@@ -24,6 +24,26 @@
 //   k_flush applies whatever is still pending (readback, end of a solve).
 //
 //   x_b, c_B, b (L), c (n), alpha[2], ybuf[2] (L), b_ixs (m int64).
+//
+// Eta window (Params::win = KW > 0).  B^-1 is not rewritten
+// every pivot.  With B stored as the window base B_w and pivots tau = 0..nw-1
+// since the last fold (nw-1 the pending one, as above):
+//   true B^-1 = B_w + sum_tau eta_tau r_tau^T, r_tau = row q_tau of B^-1 before
+//          pivot tau, eta_tau the compute_E_q column (v4:210-215) minus e_q;
+//   U      m x KW row-major, U[i*KW + tau] = eta_tau[i] (written by k_update
+//          one pass after pivot tau, from alpha and aq);
+//   Wt     (n+1) x KW, Wt[j*KW + tau] = r_tau . A_j, and Wt[n*KW + tau] =
+//          r_tau . b — written by k_price one pass after pivot tau (basic
+//          columns get their exact value: aq for the entering column, else 0),
+//          so r_tau itself is never formed: r_tau . A_j = B_w[q_tau,:] . A_j +
+//          sum_{s<tau} U[q_tau][s] Wt[j][s];
+//   y      = y_w + sum_tau SY[tau] r_tau, so e_j = y_w . A_j + sum SY[tau]
+//          Wt[j][tau] - c_j; alpha = B_w A_p + sum U[:,tau] Wt[p][tau];
+//   Qrows/Urows  the base rows B_w[q_tau,:] and coefficients U[q_tau][s<tau]
+//          (staged by k_price) from which k_fold rebuilds the r_tau.
+// When nw reaches KW, k_fold folds the nw-1 complete pivots into B_w and y_w
+// (rank-(KW-1) update, read + write of B once) and the pending pivot becomes
+// tau = 0.
 //   nb_list / nb_pos   this rank's non-basic columns (compact list + position,
 //          swap-remove / append per pivot) so pricing touches non-basic
 //          columns only.
@@ -32,7 +52,7 @@
 
 namespace spx {
 
-enum : int32_t { ST_RUNNING = 0, ST_OPTIMAL = 1, ST_UNBOUNDED = 2 };
+enum : int32_t { ST_RUNNING = 0, ST_OPTIMAL = 1, ST_UNBOUNDED = 2, ST_WINDOW_FULL = 16 };
 
 // (value, global index) candidate; the order is value, then smallest index —
 // cub::DeviceReduce::ArgMin's first-index semantics (v4:294,324) for every
@@ -46,6 +66,15 @@ struct alignas(16) ArgMinEntry {
 // index on ties) with that row's alpha / c_B / b_ixs, the count of
 // alpha_i <= 0, and T = sum of c_B[i] * alpha_i over its rows — everything
 // the pivot needs, so the last workgroup's tail is one round trip.
+// Pricing partial of one k_price workgroup: its entering candidate and, in the
+// eta window, that column's new Wt entry.
+struct alignas(16) PricePartial {
+    double val;
+    int64_t idx;
+    double w;
+    double pad;
+};
+
 struct alignas(16) UpdPartial {
     double theta;
     int64_t idx;
@@ -88,7 +117,10 @@ struct alignas(16) DevState {
     int32_t y_buf;
     uint32_t ticket_price;
     uint32_t ticket_update;
-    int32_t pad0;
+    int32_t nw;          // eta window: pivots since the last fold (nw-1 pending)
+    uint32_t ticket_fold;
+    int32_t pad1;
+    int64_t pad2;
 };
 
 __host__ __device__ inline bool argmin_better(double v, int64_t j, double bv, int64_t bj) {
@@ -119,10 +151,12 @@ struct Params {
     // column shard of this rank: structural [s_lo, s_hi), slack [k_lo, k_hi)
     int64_t s_lo, s_hi, k_lo, k_hi;
     // reductions
-    ArgMinEntry* price_partials;
-    ArgMinEntry* price_out;        // this rank's entering candidate
-    const ArgMinEntry* price_in;   // all ranks' candidates (== price_out at 1 rank)
+    PricePartial* price_partials;
+    ArgMinEntry* price_out;        // this rank's entering candidate record
+    const ArgMinEntry* price_in;   // all ranks' records (== price_out at 1 rank)
     int32_t nin;
+    int32_t pr_stride;             // ArgMinEntry slots per record: 1, or 1 + KW/2
+                                   // (the window appends Wt[p][0..KW) to the head)
     UpdPartial* upd_partials;
     DevState* st;
     // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
@@ -136,6 +170,14 @@ struct Params {
     // diagnostics (SPX_FLAG_STAMPS): per kernel {min WG start, sum body, sum tail}
     // in s_memrealtime ticks (100 MHz); nullptr in normal runs
     unsigned long long* stamps;
+    // eta window (see above); win = KW, 0 = explicit B^-1 updated every pivot
+    int32_t win;
+    int32_t pad_w;
+    double* U;
+    double* Wt;
+    double* Qrows;  // KW x L
+    double* Urows;  // KW x KW
+    double* SY;     // KW
 };
 
 __host__ __device__ inline bool owns_col(const Params& P, int64_t j) {

@@ -9,6 +9,7 @@ namespace spx {
 struct PriceCfg {
     int block;         // 256 / 512 / 1024 threads
     bool lds_y;        // stage y in LDS (L*8 bytes) or read it from global
+    int wm;            // 0 explicit B^-1; eta window: 1 base row in LDS, 2 in global
     size_t lds_bytes;  // dynamic LDS per workgroup
     int grid;          // workgroups (persistent-style, grid-stride over columns)
 };
@@ -32,5 +33,6 @@ hipError_t launch_tail(const Params& P, int nparts, hipStream_t s);
 hipError_t launch_materialize(const Params& P, double* out, hipStream_t s);
 hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s);
 hipError_t launch_objective(const Params& P, hipStream_t s);
+hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s);
 
 }  // namespace spx

@@ -145,10 +145,15 @@ __device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
 // ---------------------------------------------------------------------------
 // Pricing + entering argmin
 // ---------------------------------------------------------------------------
-template <int BLOCK, bool LDS_Y>
+// WM: 0 = explicit B^-1 (y updated in the LDS fill); 1 = eta window with the
+// pending base row in LDS next to y; 2 = eta window, base row read from global
+// (L2) when y and the row do not both fit.
+template <int BLOCK, bool LDS_Y, int WM>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
     constexpr int WAVES = BLOCK / 64;
+    constexpr bool WIN = WM != 0;
+    constexpr bool LDS_R = WM == 1;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -163,8 +168,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int64_t L = P.L;
     const int64_t L2 = L >> 1;
     double* ys = reinterpret_cast<double*>(smem);
-    ArgMinEntry* red = reinterpret_cast<ArgMinEntry*>(smem + (LDS_Y ? L * 8 : 0));
-    int* s_last = reinterpret_cast<int*>(red + BLOCK);
+    double* rs = reinterpret_cast<double*>(smem + (LDS_Y ? L * 8 : 0));
+    PricePartial* red =
+        reinterpret_cast<PricePartial*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0));
+    int* s_last = reinterpret_cast<int*>(red + WAVES);
     const int nb = st->nb_count;
 
     // the first CH chunks of the first column stay in flight during the y
@@ -178,107 +185,200 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&c0[lane + u * 64]);
     }
 
-    // current y = ybuf + s_y r when the last pivot's y update is pending.
-    // Workgroup 0 also persists that y and (in-place B^-1) stages the pending
-    // pivot row r for k_update.  Loads are batched YB deep per thread so the
-    // fill is one memory round trip, not one per element.
     const int64_t it = st->iter;
-    const bool pend = it > 0;
-    const bool upd_y = st->y_applied < it;
-    const double s_y = st->s_y;
+    const bool wg0 = blockIdx.x == 0;
+    constexpr int YB = 4;
     const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
+    // explicit B^-1: current y = ybuf + s_y r while the last pivot's y update is
+    // pending (workgroup 0 also persists that y and, in place, stages r for
+    // k_update).  Eta window: y_w is fixed between folds; the pending pivot's
+    // base row B_w[q,:] is staged next to it (workgroup 0 also keeps it, and
+    // U[q][s<tau], in Qrows/Urows for k_fold).  Loads are batched YB deep per
+    // thread so the fill is one memory round trip, not one per element.
+    const int KW = P.win;
+    const int nw = WIN ? st->nw : 0;
+    if (WIN && nw >= KW) {  // the host folds before this can happen
+        if (wg0 && tid == 0) st->status = ST_WINDOW_FULL;
+        return;
+    }
+    const bool pend = WIN ? nw > 0 : it > 0;
+    const int tau = nw - 1;  // pending pivot of the window
+    const bool upd_y = !WIN && st->y_applied < it;
+    const double s_y = st->s_y;
     dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
     // the pending pivot row: row q of the stored B^-1 (replicated storage), or
     // rbuf, staged by k_finalize_rs from the all-gather (row-sharded storage)
     const dbl2* rr = reinterpret_cast<const dbl2*>(
         !pend ? P.zeros
-              : (P.row_shard ? P.rbuf : ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1) + st->q * L));
-    const bool wg0 = blockIdx.x == 0;
-    const bool stage_r = SPX_INPLACE && pend && wg0 && !P.row_shard;
-    constexpr int YB = 4;
-    if (LDS_Y || wg0) {
+              : (P.row_shard ? P.rbuf : ((SPX_INPLACE || WIN || !(it & 1)) ? P.B0 : P.B1) + st->q * L));
+    const bool stage_r = WIN ? (pend && wg0) : (SPX_INPLACE && pend && wg0 && !P.row_shard);
+    if (LDS_Y || LDS_R || wg0) {
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
-        dbl2* rb = reinterpret_cast<dbl2*>(P.rbuf);
+        dbl2* rl = reinterpret_cast<dbl2*>(rs);
+        dbl2* rb = reinterpret_cast<dbl2*>(WIN ? P.Qrows + (int64_t)tau * L : P.rbuf);
+        const bool need_r = WIN ? (pend && (LDS_R || stage_r)) : (upd_y || stage_r);
         for (int64_t k0 = 0; k0 < L2; k0 += (int64_t)YB * BLOCK) {
             dbl2 yv[YB], rv[YB];
 #pragma unroll
             for (int u = 0; u < YB; ++u) {
                 const int64_t k = k0 + (int64_t)u * BLOCK + tid;
                 if (k < L2) {
-                    yv[u] = yin[k];
-                    if (upd_y || stage_r) rv[u] = rr[k];
+                    if (LDS_Y || (!WIN && wg0)) yv[u] = yin[k];
+                    if (need_r) rv[u] = rr[k];
                 }
             }
 #pragma unroll
             for (int u = 0; u < YB; ++u) {
                 const int64_t k = k0 + (int64_t)u * BLOCK + tid;
                 if (k < L2) {
-                    const dbl2 v = upd_y ? y_apply(s_y, rv[u], yv[u]) : yv[u];
-                    if constexpr (LDS_Y) yl[k] = v;
-                    if (upd_y && wg0) yout[k] = v;  // flipped in by k_update's tail
+                    if constexpr (!WIN) {
+                        const dbl2 v = upd_y ? y_apply(s_y, rv[u], yv[u]) : yv[u];
+                        if constexpr (LDS_Y) yl[k] = v;
+                        if (upd_y && wg0) yout[k] = v;  // flipped in by k_update's tail
+                    } else {
+                        if constexpr (LDS_Y) yl[k] = yv[u];
+                        if constexpr (LDS_R) {
+                            if (pend) rl[k] = rv[u];
+                        }
+                    }
                     if (stage_r) rb[k] = rv[u];
                 }
             }
         }
+        if (WIN && stage_r && tid < tau) P.Urows[(int64_t)tau * KW + tid] = P.U[st->q * KW + tid];
     }
-    if constexpr (LDS_Y) __syncthreads();
+    if constexpr (LDS_Y || LDS_R) __syncthreads();
     auto Y = [&](int64_t k) -> dbl2 {
         if constexpr (LDS_Y) return reinterpret_cast<const dbl2*>(ys)[k];
+        else if constexpr (WIN) return yin[k];
         else return upd_y ? y_apply(s_y, rr[k], yin[k]) : yin[k];
     };
+    auto Rw = [&](int64_t k) -> dbl2 {
+        if constexpr (LDS_R) return reinterpret_cast<const dbl2*>(rs)[k];
+        else return rr[k];
+    };
+    // window coefficients of this lane (lane s < tau: pivot s of the window)
+    double uq = 0.0, syl = 0.0, syp = 0.0;
+    if constexpr (WIN) {
+        if (pend) {
+            if (lane < tau) {
+                uq = P.U[st->q * KW + lane];
+                syl = P.SY[lane];
+            }
+            syp = P.SY[tau];
+        }
+    }
 
-    double best = INFINITY;
+    double best = INFINITY, bw = 0.0;
     int64_t bj = INT64_MAX;
     unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
     // consume the prefetched chunks first (same k order as the loop)
-    double p0 = 0.0, p1 = 0.0;
+    double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
     if (pre) {
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
             const dbl2 w = Y(lane + u * 64);
             p0 = fma(v0[u].x, w.x, p0);
             p1 = fma(v0[u].y, w.y, p1);
-        }
-    }
-    for (int idx = idx0; idx < nb; idx += gridDim.x * WAVES) {
-        const bool first = idx == idx0;
-        const int64_t j = first ? j0 : (int64_t)P.nb_list[idx];
-        const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
-        const bool cont = first && pre;
-        double a0 = cont ? p0 : 0.0, a1 = cont ? p1 : 0.0;
-        int64_t k = lane + (cont ? CH * 64 : 0);
-        for (; k + 7 * 64 < L2; k += 8 * 64) {
-            dbl2 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const dbl2 w = Y(k + u * 64);
-                a0 = fma(v[u].x, w.x, a0);
-                a1 = fma(v[u].y, w.y, a1);
+            if (WIN && pend) {
+                const dbl2 r = Rw(lane + u * 64);
+                q0 = fma(v0[u].x, r.x, q0);
+                q1 = fma(v0[u].y, r.y, q1);
             }
         }
-        for (; k < L2; k += 64) {
-            const dbl2 v = ld2<SPX_NT_A>(&col[k]);
-            const dbl2 w = Y(k);
-            a0 = fma(v.x, w.x, a0);
-            a1 = fma(v.y, w.y, a1);
+    }
+    // eta window: list entry nb is the pseudo-column b (r_tau . b for the
+    // pending x_b update), taken by the wave with the fewest columns
+    const int nlist = nb + ((WIN && pend) ? 1 : 0);
+    for (int idx = idx0; idx < nlist; idx += gridDim.x * WAVES) {
+        const bool first = idx == idx0;
+        const bool bcol = WIN && idx == nb;
+        const int64_t j = bcol ? P.n : (first ? j0 : (int64_t)P.nb_list[idx]);
+        const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(bcol ? P.b : P.A + j * L);
+        const bool cont = first && pre;
+        double a0 = cont ? p0 : 0.0, a1 = cont ? p1 : 0.0;
+        double b0 = cont ? q0 : 0.0, b1 = cont ? q1 : 0.0;
+        double wv = 0.0;
+        if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
+        int64_t k = lane + (cont ? CH * 64 : 0);
+        if (!WIN || !pend) {
+            for (; k + 7 * 64 < L2; k += 8 * 64) {
+                dbl2 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const dbl2 w = Y(k + u * 64);
+                    a0 = fma(v[u].x, w.x, a0);
+                    a1 = fma(v[u].y, w.y, a1);
+                }
+            }
+            for (; k < L2; k += 64) {
+                const dbl2 v = ld2<SPX_NT_A>(&col[k]);
+                const dbl2 w = Y(k);
+                a0 = fma(v.x, w.x, a0);
+                a1 = fma(v.y, w.y, a1);
+            }
+        } else {
+            for (; k + 7 * 64 < L2; k += 8 * 64) {
+                dbl2 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const dbl2 w = Y(k + u * 64);
+                    const dbl2 r = Rw(k + u * 64);
+                    a0 = fma(v[u].x, w.x, a0);
+                    a1 = fma(v[u].y, w.y, a1);
+                    b0 = fma(v[u].x, r.x, b0);
+                    b1 = fma(v[u].y, r.y, b1);
+                }
+            }
+            for (; k < L2; k += 64) {
+                const dbl2 v = ld2<SPX_NT_A>(&col[k]);
+                const dbl2 w = Y(k);
+                const dbl2 r = Rw(k);
+                a0 = fma(v.x, w.x, a0);
+                a1 = fma(v.y, w.y, a1);
+                b0 = fma(v.x, r.x, b0);
+                b1 = fma(v.y, r.y, b1);
+            }
         }
-        const double e = wave_sum(a0 + a1) - P.c[j];
-        if (argmin_better(e, j, best, bj)) { best = e; bj = j; }
+        double e, wn = 0.0;
+        if (WIN && pend) {
+            // r_tau . A_j = B_w[q,:] . A_j + sum_s U[q][s] Wt[j][s]; the window
+            // terms join the lane partials before the butterflies
+            wn = wave_sum(fma(uq, wv, b0 + b1));
+            if (lane == 0) P.Wt[j * KW + tau] = wn;
+            if (bcol) continue;
+            e = fma(syp, wn, wave_sum(fma(syl, wv, a0 + a1))) - P.c[j];
+        } else {
+            e = wave_sum(a0 + a1) - P.c[j];
+        }
+        if (argmin_better(e, j, best, bj)) { best = e; bj = j; bw = wn; }
+    }
+
+    if (WIN && pend) {
+        // the exact Wt entries of the basic columns: r_tau . A_j = aq for the
+        // entering column, 0 for the others (their B^-1 A_j is a unit vector)
+        const int64_t q = st->q;
+        const double aq = st->aq;
+        for (int64_t i = (int64_t)blockIdx.x * BLOCK + tid; i < P.m; i += (int64_t)gridDim.x * BLOCK)
+            P.Wt[P.b_ixs[i] * KW + tau] = (i == q) ? aq : 0.0;
     }
 
     stamp_stream(win, false);
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
-    if (lane == 0) red[wave] = ArgMinEntry{best, bj};
+    if (lane == 0) red[wave] = PricePartial{best, bj, bw, 0.0};
     __syncthreads();
     if (tid == 0) {
-        ArgMinEntry w = red[0];
+        PricePartial w = red[0];
         for (int i = 1; i < WAVES; ++i)
             if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
         st_agent(&P.price_partials[blockIdx.x].val, w.val);
         st_agent(&P.price_partials[blockIdx.x].idx, w.idx);
+        if constexpr (WIN) st_agent(&P.price_partials[blockIdx.x].w, w.w);
         drain_vmem();
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_price, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -289,27 +389,35 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const unsigned long long t_tail = slot ? rtime() : 0;
 
     // last workgroup: reduce all partials
-    ArgMinEntry w{INFINITY, INT64_MAX};
+    PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
     for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
         const double v = ld_agent(&P.price_partials[g].val);
         const int64_t i = ld_agent(&P.price_partials[g].idx);
-        if (argmin_better(v, i, w.val, w.idx)) w = ArgMinEntry{v, i};
+        if (argmin_better(v, i, w.val, w.idx)) w = PricePartial{v, i, WIN ? ld_agent(&P.price_partials[g].w) : 0.0, 0.0};
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const double v = __shfl_xor(w.val, off, 64);
         const int64_t i = __shfl_xor(w.idx, off, 64);
-        if (argmin_better(v, i, w.val, w.idx)) w = ArgMinEntry{v, i};
+        const double ww = __shfl_xor(w.w, off, 64);
+        if (argmin_better(v, i, w.val, w.idx)) w = PricePartial{v, i, ww, 0.0};
     }
     __syncthreads();
     if (lane == 0) red[wave] = w;
     __syncthreads();
+    PricePartial t = red[0];
+    for (int i = 1; i < WAVES; ++i)
+        if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
     if (tid == 0) {
-        ArgMinEntry t = red[0];
-        for (int i = 1; i < WAVES; ++i)
-            if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
-        *P.price_out = t;
+        P.price_out[0] = ArgMinEntry{t.val, t.idx};
         st_agent(&st->ticket_price, 0u);
+    }
+    if constexpr (WIN) {
+        // the winner's window coefficients Wt[p][0..nw) travel with it (the
+        // column may live on another rank's shard)
+        double* wo = reinterpret_cast<double*>(P.price_out + 1);
+        if (tid < KW)
+            wo[tid] = (t.idx == INT64_MAX || tid >= nw) ? 0.0 : (tid == tau ? t.w : P.Wt[t.idx * KW + tid]);
     }
     stamp_tail(slot, t_tail, win);
 }
@@ -441,8 +549,13 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
     st->nb_count = cnt;
     st->aq = aq;
     st->s_y = s_y;
-    if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
-    st->y_applied = it;
+    if (P.win) {  // eta window: the pivot joins the window as its pending entry
+        P.SY[st->nw] = s_y;
+        st->nw = st->nw + 1;
+    } else {
+        if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
+        st->y_applied = it;
+    }
     st->xb_applied = it;
     st->p = p;
     st->q = q;
@@ -481,7 +594,7 @@ template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
                                unsigned char* smem, int nparts);
 
-template <int BLOCK, int R, bool RS>
+template <int BLOCK, int R, bool RS, bool WIN>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
     if (stopped(st)) return;
@@ -497,9 +610,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // entering column: MINLOC over all ranks' candidates (v4:294-302)
     double min_e = INFINITY;
     int64_t p = INT64_MAX;
+    int gw = 0;
     for (int g = 0; g < P.nin; ++g) {
-        const ArgMinEntry e = P.price_in[g];
-        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
+        const ArgMinEntry e = P.price_in[g * P.pr_stride];
+        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
     }
     if (min_e >= -P.eps || p == INT64_MAX) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
@@ -515,14 +629,16 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
     // row-sharded storage always ping-pongs (its tail recomputes the winner
     // row from the old rows); replicated storage per SPX_INPLACE
-    constexpr bool INPL = SPX_INPLACE && !RS;
+    constexpr bool INPL = (SPX_INPLACE || WIN) && !RS;
     const double* S = INPL ? P.B0 : (par ? P.B1 : P.B0);
     const dbl2* src = reinterpret_cast<const dbl2*>(S);
     dbl2* dst = reinterpret_cast<dbl2*>(INPL ? P.B0 : (par ? P.B0 : P.B1));
     const double* a_prev = par ? P.alpha1 : P.alpha0;  // alpha of pivot it-1
     double* a_new = par ? P.alpha0 : P.alpha1;
     // the pending pivot it-1: r = S[q,:], E from a_prev and aq
-    const bool pend = it > 0;
+    const int nw = WIN ? st->nw : 0;
+    const int tau = nw - 1;  // eta window: the pending pivot
+    const bool pend = WIN ? nw > 0 : it > 0;
     const int64_t qp = st->q;
     const double aqp = st->aq;
     const double* rrow = !pend ? P.zeros : ((SPX_INPLACE || RS) ? P.rbuf : S + qp * L);
@@ -550,7 +666,63 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
-    if (nvalid == R) {
+    if constexpr (WIN) {
+        // eta window: B_w is only read; alpha_i = B_w[i,:] . A_p +
+        // sum_tau U[i][tau] Wt[p][tau], the window terms (lane tau) joining the
+        // lane partials; the pending pivot's eta column is stored into U
+        const int KW = P.win;
+        const double* wrec = reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1);
+        const double wl = lane < nw ? wrec[lane] : 0.0;
+        if (nvalid == R) {
+            constexpr int U = (R == 1) ? 8 : ((R == 2) ? 4 : 2);  // 16 dbl2 loads of B per lane in flight
+            int64_t k = lane;
+            for (; k + (U - 1) * 64 < L2; k += U * 64) {
+                dbl2 av[U], bv[U][R];
+#pragma unroll
+                for (int t = 0; t < U; ++t) {
+                    av[t] = ap[k + t * 64];
+#pragma unroll
+                    for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
+                }
+#pragma unroll
+                for (int t = 0; t < U; ++t) {
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                        acc[u] = fma(bv[t][u].x, av[t].x, acc[u]);
+                        acc[u] = fma(bv[t][u].y, av[t].y, acc[u]);
+                    }
+                }
+            }
+            for (; k < L2; k += 64) {
+                const dbl2 av = ap[k];
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    const dbl2 bv = src[base + u * L2 + k];
+                    acc[u] = fma(bv.x, av.x, acc[u]);
+                    acc[u] = fma(bv.y, av.y, acc[u]);
+                }
+            }
+        } else if (nvalid > 0) {
+            for (int64_t k = lane; k < L2; k += 64) {
+                const dbl2 av = ap[k];
+                for (int u = 0; u < nvalid; ++u) {
+                    const dbl2 bv = src[base + u * L2 + k];
+                    acc[u] = fma(bv.x, av.x, acc[u]);
+                    acc[u] = fma(bv.y, av.y, acc[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (u < nvalid) {
+                const int64_t li = lr0 + u;
+                const double cu = lane < tau ? P.U[li * KW + lane] : (lane == tau ? ei[u] : 0.0);
+                acc[u] = fma(cu, wl, acc[u]);
+                if (pend && lane == 0) P.U[li * KW + tau] = ei[u];
+            }
+        }
+        if (upd_x) sxa = P.Wt[P.n * KW + tau];
+    } else if (nvalid == R) {
         constexpr int U = (R >= 4) ? 2 : 4;
         int64_t k = lane;
         for (; k + (U - 1) * 64 < L2; k += U * 64) {
@@ -611,7 +783,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     }
 
     stamp_stream(win, false);
-    const double s_x = (upd_x && nvalid > 0) ? wave_sum(sxa) : 0.0;
+    const double s_x = (upd_x && nvalid > 0) ? (WIN ? sxa : wave_sum(sxa)) : 0.0;
 
     // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
     // (compute_theta, v4:199-208) and the wave's ratio-test partial
@@ -733,7 +905,7 @@ __global__ __launch_bounds__(1024) void k_tail(Params P, int nparts) {
     double min_e = INFINITY;
     int64_t p = INT64_MAX;
     for (int g = 0; g < P.nin; ++g) {
-        const ArgMinEntry e = P.price_in[g];
+        const ArgMinEntry e = P.price_in[g * P.pr_stride];
         if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
     }
     const int64_t it = st->iter;
@@ -756,7 +928,7 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
     double min_e = INFINITY;
     int64_t p = INT64_MAX;
     for (int g = 0; g < P.nin; ++g) {
-        const ArgMinEntry e = P.price_in[g];
+        const ArgMinEntry e = P.price_in[g * P.pr_stride];
         if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
     }
     // merge the ranks' ratio-test headers (rank order: deterministic T sum)
@@ -787,6 +959,115 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
 }
 
 // ---------------------------------------------------------------------------
+// Eta-window fold (spx_device.h): B_w += U[:, 0..nf) R, y_w += SY[0..nf) R for
+// the nf = nw - 1 complete pivots of the window; the pending pivot stays
+// pending as tau = 0.  A workgroup owns a 64-column stripe of B and a range of
+// rows.  Wave 0 rebuilds R for the stripe (one column per lane:
+// r_tau = Qrows[tau] + sum_{s<tau} Urows[tau][s] r_s) into LDS; then each wave
+// updates 16-row x 64-column tiles with v_mfma_f64_16x16x4_f64 (K = the
+// window, 4 pivots per step): the tile of B is the accumulator, U the A
+// operand, R the B operand.  B is read and written once.  min_nw: fold only
+// when nw >= min_nw (the loop asks for KW, a readback for 2).
+// ---------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
+    DevState* st = P.st;
+    const int nw = st->nw;
+    if (nw < min_nw || nw < 2) return;
+    const int nf = nw - 1;
+    constexpr int KS = KW / 4;
+    __shared__ double Rl[KW][64];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t L = P.L;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    if (wave == 0) {
+        double R[KW];
+#pragma unroll
+        for (int t = 0; t < KW; ++t) {
+            double v = 0.0;
+            if (t < nf) {
+                v = P.Qrows[(int64_t)t * L + c0 + lane];
+#pragma unroll
+                for (int s2 = 0; s2 < t; ++s2) v = fma(P.Urows[t * KW + s2], R[s2], v);
+            }
+            R[t] = v;
+            Rl[t][lane] = v;
+        }
+        if (blockIdx.y == 0) {
+            double* y = st->y_buf ? P.y1 : P.y0;
+            double d = 0.0;
+#pragma unroll
+            for (int t = 0; t < KW; ++t)
+                if (t < nf) d = fma(P.SY[t], R[t], d);
+            y[c0 + lane] += d;
+        }
+    }
+    __syncthreads();
+    // R fragments (B operand): lane holds R[4s + (lane>>4)][16 jb + (lane&15)]
+    const int kr = lane >> 4, cl = lane & 15;
+    double bf[KS][4];
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) bf[s2][jb] = Rl[4 * s2 + kr][16 * jb + cl];
+    const int ks = (nf + 3) / 4;
+    const int64_t m = P.m;
+    const int64_t per = ((m + gridDim.y - 1) / gridDim.y + 15) / 16 * 16;
+    const int64_t i0 = (int64_t)blockIdx.y * per;
+    const int64_t i1 = (i0 + per < m) ? i0 + per : m;
+    double* B = P.B0;
+    for (int64_t r0 = i0 + 16 * wave; r0 < i1; r0 += 64) {
+        // U fragment (A operand): lane holds U[r0 + (lane&15)][4s + (lane>>4)]
+        const int64_t ia = r0 + cl;
+        double af[KS];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const int t = 4 * s2 + kr;
+            af[s2] = (ia < i1 && t < nf) ? P.U[ia * KW + t] : 0.0;
+        }
+        // B tile as the accumulator: lane holds rows r0 + kr + 4 r, column 16 jb + cl
+        dbl4 acc[4];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = r0 + kr + 4 * r;
+                acc[jb][r] = (i < i1) ? B[i * L + c0 + 16 * jb + cl] : 0.0;
+            }
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            if (s2 < ks) {
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], bf[s2][jb], acc[jb], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = r0 + kr + 4 * r;
+                if (i < i1) B[i * L + c0 + 16 * jb + cl] = acc[jb][r];
+            }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_fold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (t == gridDim.x * gridDim.y - 1);
+    }
+    __syncthreads();
+    if (s_last && tid == 0) {
+        P.SY[0] = P.SY[nf];
+        st->nw = 1;
+        st_agent(&st->ticket_fold, 0u);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Deferred-state flush and readback kernels (off the hot loop)
 // ---------------------------------------------------------------------------
 // Applies the pending y and x_b updates of the last pivot (one workgroup).
@@ -796,14 +1077,18 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
     const int tid = threadIdx.x;
     const int64_t it = st->iter, L = P.L, L2 = L >> 1, m = P.m;
     if (it == 0) return;
-    const double* S = (SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1;
+    // eta window: the host folded first, so at most the pending pivot is left
+    // (nw <= 1) and the state has the explicit-B^-1 form with S = B_w
+    const double* S = (SPX_INPLACE || P.win || !(it & 1)) ? P.B0 : P.B1;
     const double* r = P.row_shard ? P.rbuf : S + st->q * L;
-    const bool upd_y = st->y_applied < it, upd_x = st->xb_applied < it;
+    const bool upd_y = P.win ? st->nw == 1 : st->y_applied < it;
+    const bool upd_x = st->xb_applied < it;
     if (upd_y) {
         const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
         dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
         const dbl2* r2 = reinterpret_cast<const dbl2*>(r);
-        for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(st->s_y, r2[k], yin[k]);
+        const double sy = P.win ? P.SY[0] : st->s_y;
+        for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(sy, r2[k], yin[k]);
     }
     if (upd_x) {
         // s_x exactly as k_update's row stream accumulates it (every wave alike)
@@ -826,6 +1111,7 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
         if (upd_y) {
             st->y_buf ^= 1;
             st->y_applied = it;
+            if (P.win) P.SY[0] = 0.0;  // y_w now includes the pending pivot
         }
         if (upd_x) st->xb_applied = it;
     }
@@ -837,7 +1123,7 @@ __global__ void k_materialize(Params P, double* out) {
     const DevState* st = P.st;
     const int64_t it = st->iter;
     const bool rs = P.row_shard != 0;
-    const double* S = rs ? ((it & 1) ? P.B1 : P.B0) : ((SPX_INPLACE || !(it & 1)) ? P.B0 : P.B1);
+    const double* S = rs ? ((it & 1) ? P.B1 : P.B0) : ((SPX_INPLACE || P.win || !(it & 1)) ? P.B0 : P.B1);
     const double* r = rs ? P.rbuf : S + st->q * P.L;
     const double* a_prev = (it & 1) ? P.alpha1 : P.alpha0;
     const int64_t q = st->q;
@@ -945,83 +1231,108 @@ __global__ void k_reset(Params P) {
         st->y_buf = 0;
         st->ticket_price = 0;
         st->ticket_update = 0;
+        st->nw = 0;
+        st->ticket_fold = 0;
     }
 }
 
 // ---------------------------------------------------------------------------
 // Host-side launchers
 // ---------------------------------------------------------------------------
-template <int BLOCK, bool LDS_Y>
+template <int BLOCK, bool LDS_Y, int WM>
 static hipError_t launch_price_t(const Params& P, int grid, size_t lds, hipStream_t s, hipEvent_t e0,
                                  hipEvent_t e1) {
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
-        hipLaunchKernelGGL((k_price<BLOCK, LDS_Y>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
     return hipGetLastError();
 }
 
-template <int BLOCK, bool LDS_Y>
+template <int BLOCK, bool LDS_Y, int WM>
 static hipError_t prep_price_t(size_t lds, int* blocks_per_cu) {
     hipError_t e = hipSuccess;
     if (lds > 65536) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_price<BLOCK, LDS_Y>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_price<BLOCK, LDS_Y, WM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_price<BLOCK, LDS_Y>, BLOCK, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_price<BLOCK, LDS_Y, WM>, BLOCK, lds);
+}
+
+// (lds_y, wm) variants: (1,0) (0,0) explicit B^-1; (1,1) (1,2) (0,2) eta window
+template <int BLOCK>
+static hipError_t price_dispatch(const PriceCfg& c, const Params* P, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                                 int* blocks_per_cu) {
+#define SPX_PV(LY, WM)                                                                  \
+    return P ? launch_price_t<BLOCK, LY, WM>(*P, c.grid, c.lds_bytes, s, e0, e1)        \
+             : prep_price_t<BLOCK, LY, WM>(c.lds_bytes, blocks_per_cu)
+    if (c.wm == 0) {
+        if (c.lds_y) SPX_PV(true, 0);
+        SPX_PV(false, 0);
+    }
+    if (c.wm == 1 && c.lds_y) SPX_PV(true, 1);
+    if (c.wm == 2) {
+        if (c.lds_y) SPX_PV(true, 2);
+        SPX_PV(false, 2);
+    }
+#undef SPX_PV
+    return hipErrorInvalidValue;
 }
 
 hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu) {
-    if (c.lds_y) {
-        switch (c.block) {
-            case 256: return prep_price_t<256, true>(c.lds_bytes, blocks_per_cu);
-            case 512: return prep_price_t<512, true>(c.lds_bytes, blocks_per_cu);
-            case 1024: return prep_price_t<1024, true>(c.lds_bytes, blocks_per_cu);
-        }
-    } else {
-        switch (c.block) {
-            case 256: return prep_price_t<256, false>(c.lds_bytes, blocks_per_cu);
-            case 512: return prep_price_t<512, false>(c.lds_bytes, blocks_per_cu);
-            case 1024: return prep_price_t<1024, false>(c.lds_bytes, blocks_per_cu);
-        }
+    switch (c.block) {
+        case 256: return price_dispatch<256>(c, nullptr, nullptr, nullptr, nullptr, blocks_per_cu);
+        case 512: return price_dispatch<512>(c, nullptr, nullptr, nullptr, nullptr, blocks_per_cu);
+        case 1024: return price_dispatch<1024>(c, nullptr, nullptr, nullptr, nullptr, blocks_per_cu);
     }
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (c.lds_y) {
-        switch (c.block) {
-            case 256: return launch_price_t<256, true>(P, c.grid, c.lds_bytes, s, e0, e1);
-            case 512: return launch_price_t<512, true>(P, c.grid, c.lds_bytes, s, e0, e1);
-            case 1024: return launch_price_t<1024, true>(P, c.grid, c.lds_bytes, s, e0, e1);
-        }
-    } else {
-        switch (c.block) {
-            case 256: return launch_price_t<256, false>(P, c.grid, c.lds_bytes, s, e0, e1);
-            case 512: return launch_price_t<512, false>(P, c.grid, c.lds_bytes, s, e0, e1);
-            case 1024: return launch_price_t<1024, false>(P, c.grid, c.lds_bytes, s, e0, e1);
-        }
+    switch (c.block) {
+        case 256: return price_dispatch<256>(c, &P, s, e0, e1, nullptr);
+        case 512: return price_dispatch<512>(c, &P, s, e0, e1, nullptr);
+        case 1024: return price_dispatch<1024>(c, &P, s, e0, e1, nullptr);
     }
     return hipErrorInvalidValue;
 }
 
-template <int BLOCK, int R, bool RS>
+template <int BLOCK, int R, bool RS, bool WIN>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = UpdLds<BLOCK>::bytes;
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
+                              P);
     } else {
-        hipLaunchKernelGGL((k_update<BLOCK, R, RS>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_update<BLOCK, R, RS, WIN>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
     return hipGetLastError();
 }
 
 template <int BLOCK, int R>
 static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    return P.row_shard ? launch_update_k<BLOCK, R, true>(P, grid, s, e0, e1)
-                       : launch_update_k<BLOCK, R, false>(P, grid, s, e0, e1);
+    if (P.row_shard) return launch_update_k<BLOCK, R, true, false>(P, grid, s, e0, e1);
+    return P.win ? launch_update_k<BLOCK, R, false, true>(P, grid, s, e0, e1)
+                 : launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
+}
+
+hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
+    const int nx = (int)(P.L / 64);
+    int64_t ny = ((int64_t)4 * cus + nx - 1) / nx;
+    const int64_t maxy = (P.m + 63) / 64;  // at least one 16-row tile per wave
+    if (ny > maxy) ny = maxy;
+    if (ny < 1) ny = 1;
+    const dim3 grid((unsigned)nx, (unsigned)ny);
+    switch (P.win) {
+        case 8: hipLaunchKernelGGL(k_fold<8>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_fold<16>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_fold<32>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_fold<64>, grid, dim3(256), 0, s, P, min_nw); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
