@@ -3,7 +3,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C2|C4|C5 | --m M --n N]
 
 A *step* is one simplex iteration (pricing over the non-basic columns, entering
-MINLOC, fused B^-1 rank-1 update + FTRAN, ratio test, x_b / y update) on the
+MINLOC, FTRAN + B^-1 update, ratio test, x_b / y update) on the
 seeded dense random LP of SURVEY.md §8(d) (default C3: m=4096, n=16384, fp64),
 with A, b, c generated directly in HBM.  W untimed iterations, then exactly K
 timed ones between barriers + device syncs; rank 0 prints one JSON line.
@@ -133,11 +133,13 @@ def main():
 
     # (1) event-timed window: per-kernel durations recorded by the dispatches
     ctx = make(timing=True)
+    cfg = ctx.config()
     dt_e, piv_e, pt, nb_local = timed_window(ctx, True)
     ctx.close()
     # (2) the same window replayed from captured hipGraphs (single rank) or
     #     launched eagerly with RCCL (multi-rank), no events
     ctx = make(timing=False)
+    cfg = ctx.config()  # the undisturbed run's geometry (graph batch included)
     dt_g, piv_g, _, _ = timed_window(ctx, False)
     ctx.close()
 
@@ -155,10 +157,15 @@ def main():
     price_ms_max, minloc_ms_max, update_ms_max = reduce_max([price_ms, minloc_ms, update_ms])
     price_bytes = 8.0 * (m + 1) * nb_local  # this rank's launch
     price_bytes_all = reduce_sum([price_bytes])[0]
-    update_bytes = 16.0 * m * m
+    # B^-1 bytes of the update launch: read + write (explicit rank-1 update),
+    # or the read-only FTRAN stream of the eta window (its fold, a read +
+    # write of B every window-1 pivots, is a separate launch)
+    win = cfg["window"]
+    update_bytes = (8.0 if win else 16.0) * m * m
     price_gbs = price_bytes / (price_ms * 1e-3) / 1e9 if price_ms > 0 else 0.0
     update_gbs = update_bytes / (update_ms * 1e-3) / 1e9 if update_ms > 0 else 0.0
-    b_alg = 8.0 * ((m + 1) * (n - m) + 2.0 * m * m)  # one iteration, whole job
+    b_upd = 8.0 * m * m * (1.0 + 2.0 / (win - 1)) if win else 16.0 * m * m
+    b_alg = 8.0 * (m + 1) * (n - m) + b_upd  # one iteration, whole job
 
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -190,7 +197,11 @@ def main():
             "data": "synthetic (seeded generator of SURVEY.md §8(d), generated in HBM)",
             "config": {
                 "workload": f"dense random LP m={m} n={n} seed={args.seed}, Dantzig revised simplex with "
-                            f"explicit B^-1 (one step = one pivot)",
+                            + (f"B^-1 as an eta window of {win} (one step = one pivot)" if win else
+                               "explicit B^-1 (one step = one pivot)"),
+                "b_inverse": (f"eta window {win}: B_w + U R, FTRAN stream read-only, rank-{win - 1} fold "
+                              f"every {win - 1} pivots" if win else "explicit, rank-1 update in place"),
+                "geometry": cfg,
                 "m": m, "n": n, "seed": args.seed,
                 "parallelism": ((f"pricing column-sharded x{world} (RCCL all-gather MINLOC), " +
                                  ("B^-1 replicated" if args.replicated else

@@ -188,10 +188,19 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
 /* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this
- * rank (8*(m+1)*local non-basic columns), bytes_update: one update launch
- * (16*m*m), as SURVEY.md §8(d). */
+ * rank (8*(m+1)*local non-basic columns), bytes_update: the B^-1 bytes per
+ * pivot — 16*m*m for the explicit rank-1 update, or
+ * 8*m*m*(1 + 2/(window-1)) for the eta window (stream + amortised fold). */
 int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
              int64_t* local_nonbasic, double* bytes_price, double* bytes_update);
+
+/* Resolved configuration: out[0] window (0 = explicit B^-1), [1] pricing
+ * threads per workgroup, [2] pricing workgroups, [3] pricing LDS mode (0 y
+ * in global, 1 y in LDS, 2 y and the window base row in LDS), [4] update
+ * threads per workgroup, [5] update rows per wave, [6] update workgroups,
+ * [7] passes per captured hipGraph (0 = eager). */
+#define SPX_CONFIG_FIELDS 8
+int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:
  * spx_shard_range: this rank's column shard — structural columns

@@ -251,6 +251,15 @@ class Context:
                 "bytes_price": bp.value, "bytes_update": bu.value}
 
 
+    def config(self):
+        """Resolved representation and launch geometry (spx_config)."""
+        out = (ctypes.c_int32 * 8)()
+        check(self._L.spx_config(self._h, out))
+        keys = ("window", "price_block", "price_grid", "price_lds", "update_block", "update_rows", "update_grid",
+                "graph_batch")
+        return dict(zip(keys, list(out)))
+
+
 def solve(A_cols, b, c, max_iter: int = (1 << 62), eps: float = 1e-7, device: int = -1) -> SolveResult:
     """Mirror of the reference's ``solve()`` (v4:219-380): A column-major as
     (n, m), returns z, status, x_b and b_ixs in basis order, pivots made."""

@@ -55,6 +55,7 @@ SIGNATURES = {
     "spx_kernel_times": (ctypes.c_int, [_p, _p, _p, _p, _p]),
     "spx_pass_times": (ctypes.c_int, [_p, _p, _p]),
     "spx_info": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p]),
+    "spx_config": (ctypes.c_int, [_p, _p]),
     "spx_phase_times": (ctypes.c_int, [_p, _p]),
     "spx_shard_range": (ctypes.c_int, [_i64, _i64, _i32, _i32, _p]),
     "spx_minloc_merge": (ctypes.c_int, [_p, _p, _i32, _p, _p]),

@@ -239,7 +239,14 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
 
     // B^-1 representation: eta window of KW pivots, or the explicit rank-1 update
     int KW = x->opts.window;
-    if (KW == 0) KW = -1;  // auto: explicit B^-1
+    if (KW == 0) {
+        // auto (measured): the window halves the B^-1 stream and
+        // costs ~5 % more pricing, so it pays once m^2 is not small against
+        // m (n - m): C3 +19 %, C5 +28 %; C4 (n = 32 m) and C2 (m = 1024,
+        // latency-bound) stay explicit.  Row-sharded B^-1 is always explicit.
+        const bool pays = m >= 2048 && (double)m >= 0.06 * (double)(n - m);
+        KW = (pays && !P.row_shard) ? 64 : -1;
+    }
     if (KW > 0 && P.row_shard) return fail(SPX_ERR_ARG, "the eta window needs replicated B^-1 (no row sharding)");
     if (KW > 0 && !(KW == 8 || KW == 16 || KW == 32 || KW == 64))
         return fail(SPX_ERR_ARG, "window must be 8, 16, 32 or 64 (got %d)", KW);
@@ -251,6 +258,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         SPX_TRY(x->alloc(&P.Qrows, (size_t)(KW * L)));
         SPX_TRY(x->alloc(&P.Urows, (size_t)(KW * KW)));
         SPX_TRY(x->alloc(&P.SY, (size_t)KW));
+        SPX_TRY(x->alloc(&P.xw, (size_t)L));
     }
     P.pr_stride = P.win ? 1 + P.win / 2 : 1;
 
@@ -298,12 +306,14 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // (C2, m=1024: 256 threads, update 20 -> 14 us)
     const int64_t rows_here = P.mloc;
     const bool big_m = rows_here > 8192;
+    // eta window (read-only stream, measured at C3): 8 waves x 1 row, 33.7 us
+    // against 36.2 us for 16 x 1 and 35.5 us for 8 x 2
     if (!(ub == 256 || ub == 512 || ub == 1024)) {
-        ub = big_m ? 512 : 1024;
+        ub = (big_m || P.win) ? 512 : 1024;
         while (ub > 256 && rows_here / (ub / 64) < x->cus) ub /= 2;
     }
     int rows = x->opts.update_rows;
-    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = big_m ? 2 : 1;
+    if (!(rows == 1 || rows == 2 || rows == 4 || rows == 8)) rows = (big_m && !P.win) ? 2 : 1;
     if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
     uc.block = ub;
     uc.rows = rows;
@@ -916,6 +926,19 @@ int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb,
     // the fold's read + write spread over its KW-1 pivots
     if (bu) *bu = x->P.win ? 8.0 * (double)x->m * (double)x->m * (1.0 + 2.0 / (x->P.win - 1))
                            : 16.0 * (double)x->m * (double)x->m;
+    return SPX_OK;
+}
+
+int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    out[0] = x->P.win;
+    out[1] = x->pcfg.block;
+    out[2] = x->pcfg.grid;
+    out[3] = !x->pcfg.lds_y ? 0 : (x->pcfg.wm == 1 ? 2 : 1);
+    out[4] = x->ucfg.block;
+    out[5] = x->ucfg.rows;
+    out[6] = x->ucfg.grid;
+    out[7] = x->batch;
     return SPX_OK;
 }
 

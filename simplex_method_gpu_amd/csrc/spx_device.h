@@ -36,7 +36,8 @@
 //          r_tau . b — written by k_price one pass after pivot tau (basic
 //          columns get their exact value: aq for the entering column, else 0),
 //          so r_tau itself is never formed: r_tau . A_j = B_w[q_tau,:] . A_j +
-//          sum_{s<tau} U[q_tau][s] Wt[j][s];
+//          sum_{s<tau} U[q_tau][s] Wt[j][s]; Wt[n*KW + tau] = r_tau . b (the
+//          pending x_b update's s_x) comes from xw = B_w b, kept by k_fold;
 //   y      = y_w + sum_tau SY[tau] r_tau, so e_j = y_w . A_j + sum SY[tau]
 //          Wt[j][tau] - c_j; alpha = B_w A_p + sum U[:,tau] Wt[p][tau];
 //   Qrows/Urows  the base rows B_w[q_tau,:] and coefficients U[q_tau][s<tau]
@@ -178,6 +179,7 @@ struct Params {
     double* Qrows;  // KW x L
     double* Urows;  // KW x KW
     double* SY;     // KW
+    double* xw;     // B_w b (L): r_tau . b = xw[q_tau] + sum_{s<tau} U[q_tau][s] Wt[n][s]
 };
 
 __host__ __device__ inline bool owns_col(const Params& P, int64_t j) {

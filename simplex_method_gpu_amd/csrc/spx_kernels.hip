@@ -52,6 +52,12 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef SPX_INPLACE
 #define SPX_INPLACE 1
 #endif
+#ifndef SPX_LDS_BATCH
+#define SPX_LDS_BATCH 4  // eta-window pricing: y / base-row LDS reads issued together
+#endif
+#ifndef SPX_WIN_U1
+#define SPX_WIN_U1 16  // eta-window FTRAN stream, 1 row per wave: dbl2 loads per lane per round trip
+#endif
 bool kernels_inplace() { return SPX_INPLACE != 0; }
 
 template <int NT>
@@ -69,6 +75,16 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
+}
+// two butterflies interleaved (their cross-lane latencies overlap)
+__device__ __forceinline__ void wave_sum2(double& a, double& b) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ta = __shfl_xor(a, off, 64);
+        const double tb = __shfl_xor(b, off, 64);
+        a += ta;
+        b += tb;
+    }
 }
 
 template <typename T>
@@ -273,35 +289,34 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     int64_t bj = INT64_MAX;
     unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
-    // consume the prefetched chunks first (same k order as the loop)
-    double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
-    if (pre) {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const dbl2 w = Y(lane + u * 64);
-            p0 = fma(v0[u].x, w.x, p0);
-            p1 = fma(v0[u].y, w.y, p1);
-            if (WIN && pend) {
-                const dbl2 r = Rw(lane + u * 64);
-                q0 = fma(v0[u].x, r.x, q0);
-                q1 = fma(v0[u].y, r.y, q1);
-            }
-        }
-    }
-    // eta window: list entry nb is the pseudo-column b (r_tau . b for the
-    // pending x_b update), taken by the wave with the fewest columns
-    const int nlist = nb + ((WIN && pend) ? 1 : 0);
-    for (int idx = idx0; idx < nlist; idx += gridDim.x * WAVES) {
+    const int nlist = nb;
+    const int stride = gridDim.x * WAVES;
+    // The first CH chunks of every column are loaded before the previous
+    // column's reduction (and, for the first column, before the LDS fill), so
+    // a wave's A stream does not stall at column boundaries.
+    bool have = pre;
+    for (int idx = idx0; idx < nlist; idx += stride) {
         const bool first = idx == idx0;
-        const bool bcol = WIN && idx == nb;
-        const int64_t j = bcol ? P.n : (first ? j0 : (int64_t)P.nb_list[idx]);
-        const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(bcol ? P.b : P.A + j * L);
-        const bool cont = first && pre;
-        double a0 = cont ? p0 : 0.0, a1 = cont ? p1 : 0.0;
-        double b0 = cont ? q0 : 0.0, b1 = cont ? q1 : 0.0;
+        const int64_t j = first ? j0 : (int64_t)P.nb_list[idx];
+        const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
         double wv = 0.0;
         if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
-        int64_t k = lane + (cont ? CH * 64 : 0);
+        double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+        int64_t k = lane;
+        if (have) {  // consume the prefetched chunks (same k order as the loop)
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const dbl2 w = Y(lane + u * 64);
+                a0 = fma(v0[u].x, w.x, a0);
+                a1 = fma(v0[u].y, w.y, a1);
+                if (WIN && pend) {
+                    const dbl2 r = Rw(lane + u * 64);
+                    b0 = fma(v0[u].x, r.x, b0);
+                    b1 = fma(v0[u].y, r.y, b1);
+                }
+            }
+            k += CH * 64;
+        }
         if (!WIN || !pend) {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
                 dbl2 v[8];
@@ -322,17 +337,25 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
         } else {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
-                dbl2 v[8];
+                dbl2 v[8], w[8], r[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
+                // LDS operands fetched SPX_LDS_BATCH elements at a time (one
+                // LDS latency per batch, not one per element)
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const dbl2 w = Y(k + u * 64);
-                    const dbl2 r = Rw(k + u * 64);
-                    a0 = fma(v[u].x, w.x, a0);
-                    a1 = fma(v[u].y, w.y, a1);
-                    b0 = fma(v[u].x, r.x, b0);
-                    b1 = fma(v[u].y, r.y, b1);
+                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
+#pragma unroll
+                    for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
+                        w[u] = Y(k + u * 64);
+                        r[u] = Rw(k + u * 64);
+                    }
+#pragma unroll
+                    for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
+                        a0 = fma(v[u].x, w[u].x, a0);
+                        a1 = fma(v[u].y, w[u].y, a1);
+                        b0 = fma(v[u].x, r[u].x, b0);
+                        b1 = fma(v[u].y, r[u].y, b1);
+                    }
                 }
             }
             for (; k < L2; k += 64) {
@@ -345,27 +368,27 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 b1 = fma(v.y, r.y, b1);
             }
         }
+        // next column's first chunks in flight during this column's reduction
+        const int nidx = idx + stride;
+        have = nidx < nlist && L2 >= CH * 64;
+        if (have) {
+            const dbl2* cn = reinterpret_cast<const dbl2*>(P.A + (int64_t)P.nb_list[nidx] * L);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&cn[lane + u * 64]);
+        }
         double e, wn = 0.0;
         if (WIN && pend) {
             // r_tau . A_j = B_w[q,:] . A_j + sum_s U[q][s] Wt[j][s]; the window
             // terms join the lane partials before the butterflies
-            wn = wave_sum(fma(uq, wv, b0 + b1));
+            double sa = fma(syl, wv, a0 + a1);
+            wn = fma(uq, wv, b0 + b1);
+            wave_sum2(sa, wn);
             if (lane == 0) P.Wt[j * KW + tau] = wn;
-            if (bcol) continue;
-            e = fma(syp, wn, wave_sum(fma(syl, wv, a0 + a1))) - P.c[j];
+            e = fma(syp, wn, sa) - P.c[j];
         } else {
             e = wave_sum(a0 + a1) - P.c[j];
         }
         if (argmin_better(e, j, best, bj)) { best = e; bj = j; bw = wn; }
-    }
-
-    if (WIN && pend) {
-        // the exact Wt entries of the basic columns: r_tau . A_j = aq for the
-        // entering column, 0 for the others (their B^-1 A_j is a unit vector)
-        const int64_t q = st->q;
-        const double aq = st->aq;
-        for (int64_t i = (int64_t)blockIdx.x * BLOCK + tid; i < P.m; i += (int64_t)gridDim.x * BLOCK)
-            P.Wt[P.b_ixs[i] * KW + tau] = (i == q) ? aq : 0.0;
     }
 
     stamp_stream(win, false);
@@ -412,9 +435,9 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         P.price_out[0] = ArgMinEntry{t.val, t.idx};
         st_agent(&st->ticket_price, 0u);
     }
-    if constexpr (WIN) {
+    if (WIN && P.nin > 1) {
         // the winner's window coefficients Wt[p][0..nw) travel with it (the
-        // column may live on another rank's shard)
+        // column may live on another rank's shard; one rank reads Wt directly)
         double* wo = reinterpret_cast<double*>(P.price_out + 1);
         if (tid < KW)
             wo[tid] = (t.idx == INT64_MAX || tid >= nw) ? 0.0 : (tid == tau ? t.w : P.Wt[t.idx * KW + tid]);
@@ -671,10 +694,32 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         // sum_tau U[i][tau] Wt[p][tau], the window terms (lane tau) joining the
         // lane partials; the pending pivot's eta column is stored into U
         const int KW = P.win;
-        const double* wrec = reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1);
+        const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
+                                       : P.Wt + p * KW;
         const double wl = lane < nw ? wrec[lane] : 0.0;
+        // s_x = r_tau . b = xw[q] + sum_{s<tau} U[q][s] Wt[n][s] (v4:347), also
+        // kept as Wt[n][tau] for later pivots and the fold
+        double sxw = 0.0;
+        if (pend) {
+            sxw = lane < tau ? P.U[qp * KW + lane] * P.Wt[P.n * KW + lane] : 0.0;
+            sxw = P.xw[qp] + wave_sum(sxw);
+            if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
+        }
+        if (pend && lane == 0) {
+            // the exact Wt entries of the basic columns for the pending pivot:
+            // r_tau . A_j = aq for its entering column, 0 for the others (their
+            // B^-1 A_j is a unit vector).  Issued before the stream so the
+            // stores retire under it.
+            const int64_t q = st->q;
+            const double aq = st->aq;
+            for (int u = 0; u < nvalid; ++u) {
+                const int64_t i = gr0 + u;
+                P.Wt[P.b_ixs[i] * KW + tau] = (i == q) ? aq : 0.0;
+            }
+        }
         if (nvalid == R) {
-            constexpr int U = (R == 1) ? 8 : ((R == 2) ? 4 : 2);  // 16 dbl2 loads of B per lane in flight
+            // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
+            constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
             int64_t k = lane;
             for (; k + (U - 1) * 64 < L2; k += U * 64) {
                 dbl2 av[U], bv[U][R];
@@ -721,7 +766,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 if (pend && lane == 0) P.U[li * KW + tau] = ei[u];
             }
         }
-        if (upd_x) sxa = P.Wt[P.n * KW + tau];
+        if (upd_x) sxa = sxw;
     } else if (nvalid == R) {
         constexpr int U = (R >= 4) ? 2 : 4;
         int64_t k = lane;
@@ -1054,6 +1099,16 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
                 if (i < i1) B[i * L + c0 + 16 * jb + cl] = acc[jb][r];
             }
     }
+    if (blockIdx.x == 0) {  // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf)
+        const double* wb = P.Wt + P.n * KW;
+        for (int64_t i = i0 + tid; i < i1; i += 256) {
+            double d = 0.0;
+#pragma unroll
+            for (int t = 0; t < KW; ++t)
+                if (t < nf) d = fma(P.U[i * KW + t], wb[t], d);
+            P.xw[i] += d;
+        }
+    }
     __syncthreads();
     if (tid == 0) {
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_fold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1205,6 +1260,7 @@ __global__ void k_reset(Params P) {
         P.x_b[i] = P.b[i];
         P.y0[i] = P.c[ns + i];
         P.b_ixs[i] = ns + i;
+        if (P.xw) P.xw[i] = P.b[i];  // B_w = I
     }
     for (int64_t j = t0; j < n; j += stride) {
         int32_t pos = -1;
