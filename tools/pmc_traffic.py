@@ -12,6 +12,9 @@ import json
 import statistics
 
 
+KERNELS = ("k_price", "k_update", "k_fold")
+
+
 def per_kernel(path, counter):
     vals = {}
     with open(path) as f:
@@ -19,7 +22,7 @@ def per_kernel(path, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row["Kernel_Name"]
-            key = "k_price" if "k_price" in name else ("k_update" if "k_update" in name else None)
+            key = next((k for k in KERNELS if k in name), None)
             if key:
                 vals.setdefault(key, []).append(float(row["Counter_Value"]))
     return vals
@@ -38,9 +41,10 @@ def main():
     w = per_kernel(a.write_csv, "WRITE_SIZE")
     out = {"m": a.m, "n": a.n, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes)",
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream half count), KiB -> bytes"}
-    for k in ("k_price", "k_update"):
-        fv = f.get(k, [])[a.skip:]
-        wv = w.get(k, [])[a.skip:]
+    for k in KERNELS:
+        skip = a.skip if k != "k_fold" else 0  # a fold runs once per window
+        fv = f.get(k, [])[skip:]
+        wv = w.get(k, [])[skip:]
         if not fv or not wv:
             continue
         rd = 2.0 * 1024.0 * statistics.median(fv)
