@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -123,10 +124,10 @@ struct spx_ctx {
     int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
 
     template <typename T>
-    int alloc(T** p, size_t count) {
+    int alloc(T** p, size_t count, unsigned ext_flags = ~0u) {
         void* d = nullptr;
         size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&d, bytes);
+        hipError_t e = ext_flags == ~0u ? hipMalloc(&d, bytes) : hipExtMallocWithFlags(&d, bytes, ext_flags);
         if (e != hipSuccess) return fail(SPX_ERR_OOM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
         allocs.push_back(d);
         e = hipMemsetAsync(d, 0, bytes, stream);
@@ -196,7 +197,13 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     const int64_t L = x->L;
     const int G = x->opts.nranks, r = x->opts.rank;
 
-    SPX_TRY(x->alloc(&x->A, (size_t)(L * n)));
+    {
+        // experiment (SPX_A_MEM): memory type of A — 0 default, 1 uncached, 2 fine-grained
+        const char* ev = std::getenv("SPX_A_MEM");
+        const int am = ev ? std::atoi(ev) : 0;
+        const unsigned fl = am == 1 ? hipDeviceMallocUncached : (am == 2 ? hipDeviceMallocFinegrained : ~0u);
+        SPX_TRY(x->alloc(&x->A, (size_t)(L * n), fl));
+    }
     SPX_TRY(x->alloc(&x->b, (size_t)L));
     SPX_TRY(x->alloc(&x->c, (size_t)n));
 
