@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 2
+#define SPX_ABI_VERSION 3
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -55,6 +55,8 @@ extern "C" {
 #define SPX_ERR_RCCL      -4  /* an RCCL call failed                           */
 #define SPX_ERR_STATE     -5  /* call not valid in the context's state         */
 #define SPX_ERR_NO_DEVICE -6  /* no HIP device visible                         */
+#define SPX_ERR_SINGULAR  -7  /* spx_reinvert / spx_set_basis: the basis matrix
+                                 is singular (no pivot above tolerance)        */
 
 typedef struct spx_ctx spx_ctx;
 
@@ -78,8 +80,33 @@ typedef struct spx_opts {
                              B^-1 = B_w + U R kept for up to window-1 pivots,
                              then folded by one rank-(window-1) update.  The
                              window is single-shard / replicated-B^-1 only.   */
+    int32_t ratio_test;   /* leaving-row rule, SPX_RATIO_* (default REFERENCE)  */
+    int32_t refactor_every; /* spx_solve / spx_iterate: rebuild B^-1 from the
+                             basis columns (spx_reinvert) every K pivots;
+                             0 = never (the reference never does)            */
+    double  piv_tol;      /* SPX_RATIO_GUARDED / HARRIS: rows need alpha_i >
+                             piv_tol (default 1e-9)                           */
+    double  feas_tol;     /* SPX_RATIO_HARRIS: primal feasibility tolerance
+                             delta of the first pass (default 1e-9)          */
     int32_t reserved[4];
 } spx_opts;
+
+/* Leaving-row rules.
+ * REFERENCE: theta_i = x_b_i / alpha_i over alpha_i > 0, first index on ties
+ *            (compute_theta + ArgMin, v4:199-208,324); no guard, no filter.
+ * GUARDED:   only alpha_i > piv_tol (the pivot-size guard of the thesis code,
+ *            archive/thesis/cpu/liblp.c:39, gpu/culiblp.cu:401) and
+ *            theta_i = max(x_b_i, 0) / alpha_i (its x_b >= -EPS filter,
+ *            liblp.c:18-20; README.md:29-30 "x_b_t < 0", "division by a small
+ *            number").
+ * HARRIS:    two passes: theta_max = min (max(x_b_i,0) + feas_tol) / alpha_i
+ *            over alpha_i > piv_tol, then the largest alpha_i among rows with
+ *            max(x_b_i,0) / alpha_i <= theta_max (first index on ties).
+ *            Single rank or replicated B^-1 only; runs the pivot tail as its
+ *            own launch. */
+#define SPX_RATIO_REFERENCE 0
+#define SPX_RATIO_GUARDED   1
+#define SPX_RATIO_HARRIS    2
 
 #define SPX_FLAG_TIMING 1 /* record per-kernel hipEvents (spx_kernel_times)  */
 #define SPX_FLAG_STAMPS 2 /* in-kernel phase stamps (spx_phase_times); diagnostic */
@@ -129,6 +156,23 @@ int spx_group_sync(spx_ctx** ctxs, int32_t G);
 
 /* Back to the slack basis (keeps A, b, c). */
 int spx_reset(spx_ctx* ctx);
+
+/* Rebuild B^-1 from the current basis columns of A on the device (pivot-in
+ * reinversion, 64-column MFMA blocks; procedure: oracle/simplex_oracle.h
+ * orc_reinvert) and recompute x_b = B^-1 b, y = c_B B^-1 (the v2 formulas,
+ * v2_quadratic_B_inv.cu:337-338,396-397).  The basis order is kept.  Also
+ * run every opts.refactor_every pivots by spx_iterate / spx_solve.  Replicated
+ * B^-1 only (not with SPX_FLAG_ROW_SHARD).  SPX_ERR_SINGULAR when the basis
+ * matrix has no pivot above 1e-11 of a column's largest entry.  With
+ * nranks > 1 every rank must call it (no communication; the results are
+ * bit-identical). */
+int spx_reinvert(spx_ctx* ctx);
+
+/* Warm start: make basis[0..m) (distinct column indices, basis order) the
+ * current basis, B^-1 by reinversion, status back to running (pivot count
+ * kept).  The primal simplex needs x_b = B^-1 b >= 0: read x_b back to check.
+ * On SPX_ERR_SINGULAR the context has no valid basis until spx_reset. */
+int spx_set_basis(spx_ctx* ctx, const int64_t* basis);
 
 /* Whole solve, device-resident: at most max_iter loop passes (reference
  * MAX_ITER, v4:19, do/while at v4:286-359).  Writes z, x_b[m], b_ixs[m] (basis

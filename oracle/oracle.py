@@ -28,6 +28,15 @@ MAX_ITER, OPTIMUM_FOUND, UNBOUNDED, THETA_OVERFLOW = 0, 1, 2, 3
 
 _lib = None
 
+# leaving-row rules (include/simplex.h SPX_RATIO_*)
+RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
+
+
+class OrcOpts(ctypes.Structure):
+    _fields_ = [("max_iter", ctypes.c_int64), ("eps", ctypes.c_double), ("threads", ctypes.c_int),
+                ("ratio", ctypes.c_int), ("piv_tol", ctypes.c_double), ("feas_tol", ctypes.c_double),
+                ("refactor_every", ctypes.c_int64)]
+
 
 def build() -> str:
     import subprocess
@@ -56,6 +65,13 @@ def lib() -> ctypes.CDLL:
         L.orc_time_iterations.restype = d
         L.orc_price.argtypes = [i64, i64, p, p, p, p, ctypes.c_int]
         L.orc_price.restype = None
+        L.orc_solve_ex.argtypes = [i64, i64, p, p, p, ctypes.POINTER(OrcOpts),
+                                   p, p, p, p, p, p, i64, p, p]
+        L.orc_solve_ex.restype = ctypes.c_int
+        L.orc_default_opts.argtypes = [ctypes.POINTER(OrcOpts)]
+        L.orc_default_opts.restype = None
+        L.orc_reinvert.argtypes = [i64, i64, p, p, p, p, ctypes.c_int, p, p, p]
+        L.orc_reinvert.restype = ctypes.c_int
         L.orc_max_threads.argtypes = []
         L.orc_max_threads.restype = ctypes.c_int
         _lib = L
@@ -155,7 +171,8 @@ class OracleResult:
 
 def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 << 40,
           eps: float = 1e-7, threads: int = 0, trace_cap: int = 0,
-          want_state: bool = False) -> OracleResult:
+          want_state: bool = False, ratio: int = RATIO_REFERENCE, piv_tol: float = 1e-9,
+          feas_tol: float = 1e-9, refactor_every: int = 0) -> OracleResult:
     n, m = A_cols.shape
     A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
@@ -168,13 +185,34 @@ def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 <<
     tq = np.full(max(trace_cap, 1), -1, dtype=np.int64)
     y = np.zeros(m) if want_state else None
     binv = np.zeros((m, m)) if want_state else None
-    st = lib().orc_solve(m, n, _ptr(A_cols), _ptr(b), _ptr(c), max_iter, eps, threads,
-                         ctypes.byref(z), _ptr(x_b), _ptr(b_ixs), ctypes.byref(piv),
-                         _ptr(tp), _ptr(tq), trace_cap, _ptr(y), _ptr(binv))
+    o = OrcOpts()
+    lib().orc_default_opts(ctypes.byref(o))
+    o.max_iter, o.eps, o.threads = max_iter, eps, threads
+    o.ratio, o.piv_tol, o.feas_tol, o.refactor_every = ratio, piv_tol, feas_tol, refactor_every
+    st = lib().orc_solve_ex(m, n, _ptr(A_cols), _ptr(b), _ptr(c), ctypes.byref(o),
+                            ctypes.byref(z), _ptr(x_b), _ptr(b_ixs), ctypes.byref(piv),
+                            _ptr(tp), _ptr(tq), trace_cap, _ptr(y), _ptr(binv))
     if st < 0:
         raise ValueError(f"orc_solve failed ({st})")
     k = min(piv.value, trace_cap)
     return OracleResult(st, z.value, x_b, b_ixs, piv.value, tp[:k], tq[:k], y, binv)
+
+
+def reinvert(A_cols, b, c, basis, threads: int = 0):
+    """Pivot-in reinversion of the basis (orc_reinvert): (B^-1 row-major, x_b, y)
+    in the given basis order.  Raises ValueError on a bad or singular basis."""
+    n, m = A_cols.shape
+    basis = np.ascontiguousarray(basis, dtype=np.int64)
+    binv = np.zeros((m, m))
+    x_b = np.zeros(m)
+    y = np.zeros(m)
+    rc = lib().orc_reinvert(m, n, _ptr(np.ascontiguousarray(A_cols, dtype=np.float64)),
+                            _ptr(np.ascontiguousarray(b, dtype=np.float64)),
+                            _ptr(np.ascontiguousarray(c, dtype=np.float64)), _ptr(basis), threads,
+                            _ptr(binv), _ptr(x_b), _ptr(y))
+    if rc != 0:
+        raise ValueError(f"orc_reinvert failed ({rc}: {'singular basis' if rc == -7 else 'bad basis'})")
+    return binv, x_b, y
 
 
 def price(A_cols, c, y, threads: int = 0) -> np.ndarray:

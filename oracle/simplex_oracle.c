@@ -139,8 +139,50 @@ static void state_free(orc_state* s) {
 
 /* One pass of the do-loop body (v4:286-357).  Returns ORC_MAX_ITER when a
  * pivot was made (loop continues), otherwise the terminating status. */
+/* Leaving row under the SPX_RATIO_* rules (include/simplex.h).  rule 0 is the
+ * reference: compute_theta (v4:199-208, strict alpha_i > 0, no filter) + the
+ * first-index ArgMin (v4:324-325).  Returns -1 when no row is a candidate
+ * (Unbounded, v4:317-322). */
+static int64_t ratio_test(const orc_state* s, int rule, double piv_tol,
+                          double feas_tol) {
+    const int64_t m = s->m;
+    const double pt = rule == 0 ? 0.0 : piv_tol;
+    int64_t non_pos = 0;
+    for (int64_t i = 0; i < m; ++i) {
+        const double a = s->alpha[i], xb = s->x_b[i];
+        const int flag = a > pt;
+        double th = INFINITY;
+        if (flag) {
+            if (rule == 0) th = xb / a;
+            else {
+                const double xc = xb > 0.0 ? xb : 0.0;
+                th = rule == 2 ? (xc + feas_tol) / a : xc / a;
+            }
+        }
+        s->theta[i] = th;
+        non_pos += !flag;
+    }
+    if (non_pos == m) return -1;
+    double thmax;
+    int64_t q = argmin_first(s->theta, m, &thmax);
+    if (rule == 2) {
+        /* Harris second pass: largest alpha_i among rows whose clamped ratio
+         * is within theta_max, first index on ties */
+        double best = -INFINITY;
+        q = -1;
+        for (int64_t i = 0; i < m; ++i) {
+            const double a = s->alpha[i];
+            if (!(a > pt)) continue;
+            const double xc = s->x_b[i] > 0.0 ? s->x_b[i] : 0.0;
+            if (xc / a <= thmax && a > best) { best = a; q = i; }
+        }
+    }
+    return q;
+}
+
 static int one_pass(orc_state* s, const double* A, const double* b,
-                    const double* c, double eps, int64_t* p_out, int64_t* q_out) {
+                    const double* c, double eps, int rule, double piv_tol,
+                    double feas_tol, int64_t* p_out, int64_t* q_out) {
     const int64_t m = s->m, n = s->n;
     double min_val;
 
@@ -165,17 +207,9 @@ static int one_pass(orc_state* s, const double* A, const double* b,
         for (int64_t i = i0; i < i1; ++i) s->alpha[i] = acc[i - i0];
     }
 
-    /* compute_theta (v4:199-208): strict alpha_i > 0, no pivot tolerance */
-    int64_t non_pos = 0;
-    for (int64_t i = 0; i < m; ++i) {
-        const int flag = s->alpha[i] > 0;
-        s->theta[i] = flag ? s->x_b[i] / s->alpha[i] : INFINITY;
-        non_pos += !flag;
-    }
-    if (non_pos == m) return ORC_UNBOUNDED; /* v4:317-322 */
-
-    /* leaving ArgMin (v4:324-325) */
-    const int64_t q = argmin_first(s->theta, m, &min_val);
+    /* compute_theta + leaving ArgMin (v4:199-208,317-325), or a variant */
+    const int64_t q = ratio_test(s, rule, piv_tol, feas_tol);
+    if (q < 0) return ORC_UNBOUNDED;
 
     /* r = B_inv[q,:] (cublasScopy, v4:331); E_q (compute_E_q v4:210-215) */
     for (int64_t k = 0; k < m; ++k) s->r[k] = s->Binv[q + k * m];
@@ -214,28 +248,147 @@ static int one_pass(orc_state* s, const double* A, const double* b,
     return ORC_MAX_ITER;
 }
 
-int orc_solve(int64_t m, int64_t n, const double* A, const double* b,
-              const double* c, int64_t max_iter, double eps, int threads,
-              double* z, double* x_b, int64_t* b_ixs, int64_t* pivots,
-              int64_t* trace_p, int64_t* trace_q, int64_t trace_cap,
-              double* y_out, double* binv_out) {
-    if (m <= 0 || n < m) return -1; /* CLI rejects m > n (v4:402-405) */
+/* Pivot-in reinversion (orc_reinvert).  Binv_cm: m x m COLUMN-major output
+ * (the oracle's layout), already in the given basis order. */
+static int reinvert_core(int64_t m, int64_t n, const double* A,
+                         const int64_t* basis, double* Binv_cm) {
+    const int64_t ns = n - m;
+    double* X = (double*)malloc(sizeof(double) * (size_t)(m * m)); /* col-major */
+    double* alpha = (double*)malloc(sizeof(double) * (size_t)m);
+    double* eta = (double*)malloc(sizeof(double) * (size_t)m);
+    double* xq = (double*)malloc(sizeof(double) * (size_t)m);
+    int64_t* owner = (int64_t*)malloc(sizeof(int64_t) * (size_t)m); /* row -> basis position */
+    char* seen = (char*)calloc((size_t)n, 1);
+    int rc = 0;
+    if (!X || !alpha || !eta || !xq || !owner || !seen) { rc = -2; goto out; }
+    for (int64_t k = 0; k < m; ++k) {
+        if (basis[k] < 0 || basis[k] >= n || seen[basis[k]]) { rc = -1; goto out; }
+        seen[basis[k]] = 1;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < m; ++k)
+        for (int64_t i = 0; i < m; ++i) X[i + k * m] = (i == k) ? 1.0 : 0.0;
+    for (int64_t i = 0; i < m; ++i) owner[i] = -1;
+    for (int64_t k = 0; k < m; ++k) /* slack columns keep their rows */
+        if (basis[k] >= ns) owner[basis[k] - ns] = k;
+    for (int64_t k = 0; k < m; ++k) {
+        const int64_t j = basis[k];
+        if (j >= ns) continue;
+        const double* Aj = A + j * m;
+        /* alpha = X A_j (FTRAN) */
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < m; ++i) {
+            double acc = 0.0;
+            for (int64_t l = 0; l < m; ++l) acc += X[i + l * m] * Aj[l];
+            alpha[i] = acc;
+        }
+        double amax = 0.0, best = -1.0;
+        int64_t q = -1;
+        for (int64_t i = 0; i < m; ++i) {
+            const double v = fabs(alpha[i]);
+            if (v > amax) amax = v;
+            if (owner[i] < 0 && v > best) { best = v; q = i; }
+        }
+        if (q < 0 || !(best > 1e-11 * amax)) { rc = -7; goto out; }
+        const double aq = alpha[q];
+        for (int64_t i = 0; i < m; ++i) eta[i] = (i != q) ? -alpha[i] / aq : 1.0 / aq - 1.0;
+        for (int64_t l = 0; l < m; ++l) xq[l] = X[q + l * m];
+#pragma omp parallel for schedule(static)
+        for (int64_t l = 0; l < m; ++l) {
+            const double r = xq[l];
+            double* col = X + l * m;
+            for (int64_t i = 0; i < m; ++i) col[i] += eta[i] * r;
+        }
+        owner[q] = k;
+    }
+    /* B^-1[k,:] = X[row owned by k,:] */
+    for (int64_t i = 0; i < m; ++i) {
+        const int64_t k = owner[i];
+        for (int64_t l = 0; l < m; ++l) Binv_cm[k + l * m] = X[i + l * m];
+    }
+out:
+    free(X); free(alpha); free(eta); free(xq); free(owner); free(seen);
+    return rc;
+}
+
+/* x_b = B^-1 b and y = c_B B^-1 from a column-major B^-1 (the v2 formulas,
+ * v2_quadratic_B_inv.cu:337-338,396-397). */
+static void basis_vectors(int64_t m, const double* Binv_cm, const double* b,
+                          const double* c_b, double* x_b, double* y) {
+    for (int64_t i = 0; i < m; ++i) x_b[i] = 0.0;
+    for (int64_t l = 0; l < m; ++l) {
+        const double* col = Binv_cm + l * m;
+        for (int64_t i = 0; i < m; ++i) x_b[i] += col[i] * b[l];
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t l = 0; l < m; ++l) {
+        const double* col = Binv_cm + l * m;
+        double acc = 0.0;
+        for (int64_t i = 0; i < m; ++i) acc += c_b[i] * col[i];
+        y[l] = acc;
+    }
+}
+
+int orc_reinvert(int64_t m, int64_t n, const double* A, const double* b,
+                 const double* c, const int64_t* basis, int threads,
+                 double* binv_out, double* x_b, double* y) {
+    if (m <= 0 || n < m) return -1;
     set_threads(threads);
+    double* Bi = (double*)malloc(sizeof(double) * (size_t)(m * m));
+    double* cb = (double*)malloc(sizeof(double) * (size_t)m);
+    double* xb = (double*)malloc(sizeof(double) * (size_t)m);
+    double* yy = (double*)malloc(sizeof(double) * (size_t)m);
+    int rc = (Bi && cb && xb && yy) ? reinvert_core(m, n, A, basis, Bi) : -2;
+    if (rc == 0) {
+        for (int64_t k = 0; k < m; ++k) cb[k] = c[basis[k]];
+        basis_vectors(m, Bi, b, cb, xb, yy);
+        if (x_b) memcpy(x_b, xb, sizeof(double) * (size_t)m);
+        if (y) memcpy(y, yy, sizeof(double) * (size_t)m);
+        if (binv_out)
+            for (int64_t r = 0; r < m; ++r)
+                for (int64_t k = 0; k < m; ++k) binv_out[r * m + k] = Bi[r + k * m];
+    }
+    free(Bi); free(cb); free(xb); free(yy);
+    return rc;
+}
+
+void orc_default_opts(orc_opts* o) {
+    o->max_iter = (int64_t)1 << 40;
+    o->eps = 1e-7;
+    o->threads = 0;
+    o->ratio = 0;
+    o->piv_tol = 1e-9;
+    o->feas_tol = 1e-9;
+    o->refactor_every = 0;
+}
+
+int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
+                 const double* c, const orc_opts* o, double* z, double* x_b,
+                 int64_t* b_ixs, int64_t* pivots, int64_t* trace_p,
+                 int64_t* trace_q, int64_t trace_cap, double* y_out,
+                 double* binv_out) {
+    if (m <= 0 || n < m) return -1; /* CLI rejects m > n (v4:402-405) */
+    set_threads(o->threads);
     orc_state s;
     if (state_init(&s, m, n, b, c) != 0) { state_free(&s); return -2; }
 
     int status = ORC_MAX_ITER;
     int64_t i = 0;
-    if (max_iter > 0) {
+    if (o->max_iter > 0) {
         do { /* v4:286-359 */
             int64_t p = -1, q = -1;
-            status = one_pass(&s, A, b, c, eps, &p, &q);
+            status = one_pass(&s, A, b, c, o->eps, o->ratio, o->piv_tol, o->feas_tol, &p, &q);
             if (status != ORC_MAX_ITER) break;
             if (i < trace_cap) {
                 if (trace_p) trace_p[i] = p;
                 if (trace_q) trace_q[i] = q;
             }
-        } while (++i < max_iter);
+            if (o->refactor_every > 0 && (i + 1) % o->refactor_every == 0) {
+                const int rc = reinvert_core(m, n, A, s.b_ixs, s.Binv);
+                if (rc != 0) { state_free(&s); return rc; }
+                basis_vectors(m, s.Binv, b, s.c_b, s.x_b, s.y);
+            }
+        } while (++i < o->max_iter);
     }
 
     if (z) { /* z = c_B . x_b (cublasSdot, v4:365) */
@@ -254,6 +407,20 @@ int orc_solve(int64_t m, int64_t n, const double* A, const double* b,
     return status;
 }
 
+int orc_solve(int64_t m, int64_t n, const double* A, const double* b,
+              const double* c, int64_t max_iter, double eps, int threads,
+              double* z, double* x_b, int64_t* b_ixs, int64_t* pivots,
+              int64_t* trace_p, int64_t* trace_q, int64_t trace_cap,
+              double* y_out, double* binv_out) {
+    orc_opts o;
+    orc_default_opts(&o);
+    o.max_iter = max_iter;
+    o.eps = eps;
+    o.threads = threads;
+    return orc_solve_ex(m, n, A, b, c, &o, z, x_b, b_ixs, pivots, trace_p,
+                        trace_q, trace_cap, y_out, binv_out);
+}
+
 double orc_time_iterations(int64_t m, int64_t n, const double* A,
                            const double* b, const double* c, int64_t iters,
                            int threads, int64_t* done) {
@@ -265,7 +432,7 @@ double orc_time_iterations(int64_t m, int64_t n, const double* A,
     int64_t k = 0;
     for (; k < iters; ++k) {
         int64_t p, q;
-        if (one_pass(&s, A, b, c, -1.0e300, &p, &q) != ORC_MAX_ITER) break;
+        if (one_pass(&s, A, b, c, -1.0e300, 0, 0.0, 0.0, &p, &q) != ORC_MAX_ITER) break;
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     if (done) *done = k;

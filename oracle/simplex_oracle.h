@@ -61,6 +61,46 @@ int orc_solve(int64_t m, int64_t n, const double* A_colmajor,
               int64_t* trace_p, int64_t* trace_q, int64_t trace_cap,
               double* y_out, double* binv_out);
 
+/* Extended options, mirroring spx_opts of the product:
+ *   ratio: 0 reference (v4:199-208), 1 guarded, 2 Harris (include/simplex.h
+ *          SPX_RATIO_* has the definitions; piv_tol / feas_tol as there)
+ *   refactor_every: rebuild B^-1 from the basis columns (orc_reinvert) every
+ *          K pivots, then x_b = B^-1 b and y = c_B B^-1 (0 = never). */
+typedef struct {
+    int64_t max_iter;
+    double eps;
+    int threads;
+    int ratio;
+    double piv_tol;
+    double feas_tol;
+    int64_t refactor_every;
+} orc_opts;
+
+void orc_default_opts(orc_opts* o);
+
+/* orc_solve with orc_opts; same outputs. */
+int orc_solve_ex(int64_t m, int64_t n, const double* A_colmajor,
+                 const double* b, const double* c, const orc_opts* o,
+                 double* z, double* x_b, int64_t* b_ixs, int64_t* pivots,
+                 int64_t* trace_p, int64_t* trace_q, int64_t trace_cap,
+                 double* y_out, double* binv_out);
+
+/* Basis reinversion by pivoting the basis columns into the slack basis
+ * (the procedure libsimplex's spx_reinvert runs on the device):
+ *   X = I; every slack column n-m+i of the basis keeps row i; then, in basis
+ *   order, every structural column j: alpha = X A_j, q = argmax |alpha_i|
+ *   over rows not yet taken (first index on ties), singular when
+ *   |alpha_q| <= 1e-11 max_i |alpha_i|; X += eta X[q,:] with the compute_E_q
+ *   column (v4:210-215) minus e_q; row q taken by j.  Finally B^-1[k,:] =
+ *   X[row of basis[k],:], so B^-1 follows the given basis order.
+ * Requires A's last m columns to be the identity (the reference's slack
+ * assumption, v4:272-277).  Outputs (any may be NULL): binv_out ROW-major,
+ * x_b = B^-1 b, y = c_B B^-1 (c_B[k] = c[basis[k]]).  Returns 0, -1 on bad
+ * input (index out of range / repeated), -7 when singular. */
+int orc_reinvert(int64_t m, int64_t n, const double* A_colmajor,
+                 const double* b, const double* c, const int64_t* basis,
+                 int threads, double* binv_out, double* x_b, double* y);
+
 /* Timed sample for the CPU baseline: runs `iters` pivots from the slack basis
  * and returns wall seconds of the iteration loop only (steady clock). */
 double orc_time_iterations(int64_t m, int64_t n, const double* A_colmajor,

@@ -24,13 +24,16 @@ from ._lib import SimplexError, SpxOpts, check, load
 
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
            "shard_range", "minloc_merge", "group_iterate", "group_sync",
-           "SimplexError", "FLAG_TIMING"]
+           "SimplexError", "FLAG_TIMING", "RATIO_REFERENCE", "RATIO_GUARDED", "RATIO_HARRIS"]
 
 FLAG_TIMING = 1
 FLAG_STAMPS = 2
 FLAG_GLOBAL_Y = 4
 FLAG_ROW_SHARD = 8
 FLAG_SPLIT_TAIL = 16
+
+# leaving-row rules (include/simplex.h SPX_RATIO_*)
+RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
 
 
 class SolveStatus(IntEnum):
@@ -118,7 +121,8 @@ class Context:
                  seed: int | None = None, eps: float = 1e-7, device: int = -1, rank: int = 0,
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
-                 global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0):
+                 global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
+                 ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -126,6 +130,8 @@ class Context:
         o.graph_batch, o.price_block, o.update_rows, o.price_grid = graph_batch, price_block, update_rows, price_grid
         o.update_block = update_block
         o.window = window  # 0 auto, -1 explicit rank-1 B^-1 update, 8/16/32/64 eta window
+        o.ratio_test, o.piv_tol, o.feas_tol = ratio_test, piv_tol, feas_tol  # RATIO_*
+        o.refactor_every = refactor_every
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
                    | (FLAG_SPLIT_TAIL if split_tail else 0))
@@ -171,6 +177,17 @@ class Context:
 
     def reset(self):
         check(self._L.spx_reset(self._h))
+
+    def reinvert(self):
+        """Rebuild B^-1 (and x_b, y) from the current basis columns (spx_reinvert)."""
+        check(self._L.spx_reinvert(self._h))
+
+    def set_basis(self, basis):
+        """Warm start from ``basis`` (m distinct column indices, basis order)."""
+        bs = np.ascontiguousarray(basis, dtype=np.int64)
+        if bs.shape != (self.m,):
+            raise ValueError(f"basis must have {self.m} entries")
+        check(self._L.spx_set_basis(self._h, _ptr(bs)))
 
     # -- loop
     def iterate(self, k: int):

@@ -31,6 +31,10 @@ class SpxOpts(ctypes.Structure):
         ("flags", ctypes.c_int32),
         ("update_block", ctypes.c_int32),
         ("window", ctypes.c_int32),
+        ("ratio_test", ctypes.c_int32),
+        ("refactor_every", ctypes.c_int32),
+        ("piv_tol", ctypes.c_double),
+        ("feas_tol", ctypes.c_double),
         ("reserved", ctypes.c_int32 * 4),
     ]
 
@@ -43,6 +47,8 @@ SIGNATURES = {
     "spx_comm_unique_id": (ctypes.c_int, [_p]),
     "spx_attach_comm": (ctypes.c_int, [_p, _p]),
     "spx_reset": (ctypes.c_int, [_p]),
+    "spx_reinvert": (ctypes.c_int, [_p]),
+    "spx_set_basis": (ctypes.c_int, [_p, _p]),
     "spx_group_iterate": (ctypes.c_int, [_p, _i32, _i64, _p, _p]),
     "spx_group_sync": (ctypes.c_int, [_p, _i32]),
     "spx_solve": (ctypes.c_int, [_p, _i64, _p, _p, _p, _p, _p]),

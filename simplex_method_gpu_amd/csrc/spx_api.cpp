@@ -21,6 +21,7 @@
 #include "../../include/simplex.h"
 #include "spx_device.h"
 #include "spx_kernels.h"
+#include "spx_reinv.h"
 
 using namespace spx;
 
@@ -123,6 +124,16 @@ struct spx_ctx {
     bool stepped_price = false;
     int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
 
+    // basis reinversion (spx_reinv.h): work buffers allocated on first use
+    RvParams rv{};
+    double* rv_Pa = nullptr;
+    double* rv_Pb = nullptr;
+    double* rv_Ypart = nullptr;
+    int64_t* rv_cols = nullptr;
+    int64_t* rv_pos = nullptr;
+    int64_t refactor_base = 0;  // pivots at the last reinversion (opts.refactor_every)
+    bool broken = false;        // a failed spx_set_basis left no valid basis
+
     template <typename T>
     int alloc(T** p, size_t count, unsigned ext_flags = ~0u) {
         void* d = nullptr;
@@ -147,6 +158,10 @@ void spx_default_opts(spx_opts* o) {
     o->rank = 0;
     o->nranks = 1;
     o->graph_batch = 0;
+    o->ratio_test = SPX_RATIO_REFERENCE;
+    o->refactor_every = 0;
+    o->piv_tol = 1e-9;
+    o->feas_tol = 1e-9;
 }
 
 const char* spx_last_error(void) { return g_err.c_str(); }
@@ -219,7 +234,19 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // row shard of B^-1 (SPX_FLAG_ROW_SHARD with nranks > 1): rows
     // [r0, r0 + mloc), ping-pong storage; otherwise all rows, in place
     P.row_shard = (G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD)) ? 1 : 0;
-    P.split_tail = (x->opts.flags & SPX_FLAG_SPLIT_TAIL) ? 1 : 0;
+    // leaving-row rule (SPX_RATIO_*); Harris runs its second pass in k_tail
+    const int rule = x->opts.ratio_test;
+    if (rule != SPX_RATIO_REFERENCE && rule != SPX_RATIO_GUARDED && rule != SPX_RATIO_HARRIS)
+        return fail(SPX_ERR_ARG, "bad ratio_test %d", rule);
+    if (rule != SPX_RATIO_REFERENCE && !(x->opts.piv_tol >= 0.0)) return fail(SPX_ERR_ARG, "piv_tol must be >= 0");
+    if (rule == SPX_RATIO_HARRIS && !(x->opts.feas_tol >= 0.0)) return fail(SPX_ERR_ARG, "feas_tol must be >= 0");
+    if (rule == SPX_RATIO_HARRIS && G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD))
+        return fail(SPX_ERR_ARG, "the Harris ratio test needs replicated B^-1 (no row sharding)");
+    if (x->opts.refactor_every < 0) return fail(SPX_ERR_ARG, "refactor_every must be >= 0");
+    P.ratio = rule;
+    P.piv_tol = rule == SPX_RATIO_REFERENCE ? 0.0 : x->opts.piv_tol;
+    P.feas_tol = rule == SPX_RATIO_HARRIS ? x->opts.feas_tol : 0.0;
+    P.split_tail = ((x->opts.flags & SPX_FLAG_SPLIT_TAIL) || rule == SPX_RATIO_HARRIS) ? 1 : 0;
     x->mb = P.row_shard ? (m + G - 1) / G : m;
     P.r0 = P.row_shard ? std::min<int64_t>(m, (int64_t)r * x->mb) : 0;
     P.mloc = P.row_shard ? std::min<int64_t>(m, P.r0 + x->mb) - P.r0 : m;
@@ -493,7 +520,27 @@ int set_limit(spx_ctx* x, int64_t limit) {
     return SPX_OK;
 }
 
+int iterate_raw(spx_ctx* x, int64_t k);
+int reinvert_current(spx_ctx* x);
+
+// k passes, with a basis reinversion every opts.refactor_every pivots
 int iterate(spx_ctx* x, int64_t k) {
+    if (x->broken) return fail(SPX_ERR_STATE, "no valid basis (a failed spx_set_basis): call spx_reset");
+    const int64_t K = x->opts.refactor_every;
+    if (K <= 0) return iterate_raw(x, k);
+    int64_t left = k;
+    while (left > 0 && x->status == SPX_STATUS_MAX_ITER) {
+        const int64_t chunk = std::min(left, std::max<int64_t>(1, x->refactor_base + K - x->pivots));
+        const int64_t before = x->pivots;
+        SPX_TRY(iterate_raw(x, chunk));
+        left -= chunk;
+        if (x->pivots == before) break;
+        if (x->status == SPX_STATUS_MAX_ITER && x->pivots - x->refactor_base >= K) SPX_TRY(reinvert_current(x));
+    }
+    return SPX_OK;
+}
+
+int iterate_raw(spx_ctx* x, int64_t k) {
     if (x->status != SPX_STATUS_MAX_ITER || k <= 0) return SPX_OK;
     if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
     SPX_TRY(set_limit(x, x->pivots + k));
@@ -514,6 +561,108 @@ int iterate(spx_ctx* x, int64_t k) {
     }
     for (int64_t i = 0; i < left; ++i) SPX_TRY(enqueue_pass(x, x->timing));
     return read_state(x);
+}
+
+// ---------------------------------------------------------------------------
+// Basis reinversion (spx_reinv.h)
+// ---------------------------------------------------------------------------
+int rv_prepare(spx_ctx* x) {
+    if (x->rv.X) return SPX_OK;
+    RvParams& R = x->rv;
+    const int64_t m = x->m, L = x->L;
+    R.A = x->A;
+    R.m = m;
+    R.L = L;
+    const int64_t tiles = (m + 63) / 64;
+    int64_t S = std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, L / 32));
+    R.ks = round_up((L + S - 1) / S, 32);
+    R.S = (int32_t)((L + R.ks - 1) / R.ks);
+    SPX_TRY(x->alloc(&R.X, (size_t)(m * L)));
+    SPX_TRY(x->alloc(&R.Ppart, (size_t)(R.S * RV_NB * L)));
+    SPX_TRY(x->alloc(&x->rv_Pa, (size_t)(RV_NB * L)));
+    SPX_TRY(x->alloc(&x->rv_Pb, (size_t)(RV_NB * L)));
+    SPX_TRY(x->alloc(&R.U, (size_t)(m * RV_NB)));
+    SPX_TRY(x->alloc(&R.Qrows, (size_t)(RV_NB * L)));
+    SPX_TRY(x->alloc(&R.Urows, (size_t)(RV_NB * RV_NB)));
+    SPX_TRY(x->alloc(&R.owner, (size_t)m));
+    SPX_TRY(x->alloc(&x->rv_cols, (size_t)m));
+    SPX_TRY(x->alloc(&x->rv_pos, (size_t)m));
+    SPX_TRY(x->alloc(&R.qsel, (size_t)RV_NB));
+    SPX_TRY(x->alloc(&R.parts, (size_t)rv_select_grid(m)));
+    SPX_TRY(x->alloc(&R.rs, 1));
+    SPX_TRY(x->alloc(&x->rv_Ypart, (size_t)(rv_y_splits(m) * L)));
+    return SPX_OK;
+}
+
+// Rebuild B^-1 (and x_b, c_B, y) for `basis` (m distinct columns, basis order)
+// on the device; nothing is left pending.  Host-validated basis.
+int reinvert_basis(spx_ctx* x, const int64_t* basis) {
+    if (x->P.row_shard) return fail(SPX_ERR_STATE, "basis reinversion needs replicated B^-1 (no row sharding)");
+    SPX_TRY(rv_prepare(x));
+    RvParams& R = x->rv;
+    const int64_t m = x->m, ns = x->ns, L = x->L;
+    std::vector<int32_t> owner((size_t)m, -1);
+    std::vector<int64_t> cols, pos;
+    for (int64_t k = 0; k < m; ++k) {
+        if (basis[k] >= ns) owner[(size_t)(basis[k] - ns)] = (int32_t)k;  // slacks keep their rows
+        else { cols.push_back(basis[k]); pos.push_back(k); }
+    }
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(R.owner, owner.data(), (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (!cols.empty()) {
+        HIP_TRY(hipMemcpy(x->rv_cols, cols.data(), cols.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(x->rv_pos, pos.data(), pos.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(x->P.b_ixs, basis, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync(R.rs, 0, sizeof(RvState), x->stream));
+    HIP_TRY(hipMemsetAsync(R.X, 0, (size_t)(m * L) * sizeof(double), x->stream));
+    HIP_TRY(rv_launch_identity(R, x->stream));
+    const int64_t ncols = (int64_t)cols.size();
+    for (int64_t b0 = 0; b0 < ncols; b0 += RV_NB) {
+        R.nb = (int32_t)std::min<int64_t>(RV_NB, ncols - b0);
+        R.cols = x->rv_cols + b0;
+        R.pos = x->rv_pos + b0;
+        HIP_TRY(rv_launch_gemm(R, x->stream));
+        HIP_TRY(rv_launch_reduce(R, x->rv_Pa, x->stream));
+        double* pin = x->rv_Pa;
+        double* pout = x->rv_Pb;
+        for (int tau = 0; tau < R.nb; ++tau) {
+            HIP_TRY(rv_launch_step(R, tau, pin, pout, x->stream));
+            std::swap(pin, pout);
+        }
+        HIP_TRY(rv_launch_fold(R, x->cus, x->stream));
+    }
+    RvState rs{};
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(&rs, R.rs, sizeof(rs), hipMemcpyDeviceToHost));
+    if (rs.singular)
+        return fail(SPX_ERR_SINGULAR, "singular basis: no pivot above tolerance for column %lld (basis position %lld)",
+                    (long long)basis[rs.bad_pos], (long long)rs.bad_pos);
+    HIP_TRY(rv_launch_finish(x->P, R, x->rv_Ypart, x->stream));
+    x->nw = 0;
+    return read_state(x);
+}
+
+int check_basis(const spx_ctx* x, const int64_t* basis) {
+    if (!basis) return fail(SPX_ERR_ARG, "basis is NULL");
+    std::vector<char> seen((size_t)x->n, 0);
+    for (int64_t k = 0; k < x->m; ++k) {
+        const int64_t j = basis[k];
+        if (j < 0 || j >= x->n) return fail(SPX_ERR_ARG, "basis[%lld] = %lld out of range", (long long)k, (long long)j);
+        if (seen[(size_t)j]) return fail(SPX_ERR_ARG, "column %lld repeated in the basis", (long long)j);
+        seen[(size_t)j] = 1;
+    }
+    return SPX_OK;
+}
+
+int reinvert_current(spx_ctx* x) {
+    if (x->stepped_price) return fail(SPX_ERR_STATE, "reinversion between spx_price and spx_pivot");
+    std::vector<int64_t> basis((size_t)x->m);
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(basis.data(), x->P.b_ixs, (size_t)x->m * sizeof(int64_t), hipMemcpyDeviceToHost));
+    SPX_TRY(reinvert_basis(x, basis.data()));
+    x->refactor_base = x->pivots;
+    return SPX_OK;
 }
 
 int create_tail(spx_ctx* x) {
@@ -620,7 +769,47 @@ int spx_attach_comm(spx_ctx* x, const uint8_t id[SPX_COMM_ID_BYTES]) {
 
 int spx_reset(spx_ctx* x) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    x->refactor_base = 0;
+    x->broken = false;
     return do_reset(x);
+}
+
+int spx_reinvert(spx_ctx* x) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (x->broken) return fail(SPX_ERR_STATE, "no valid basis (a failed spx_set_basis): call spx_reset");
+    return reinvert_current(x);
+}
+
+int spx_set_basis(spx_ctx* x, const int64_t* basis) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_set_basis between spx_price and spx_pivot");
+    SPX_TRY(check_basis(x, basis));
+    if (x->P.row_shard) return fail(SPX_ERR_STATE, "spx_set_basis needs replicated B^-1 (no row sharding)");
+    // this rank's non-basic list (ascending, owned columns only) and positions
+    std::vector<char> basic((size_t)x->n, 0);
+    for (int64_t k = 0; k < x->m; ++k) basic[(size_t)basis[k]] = 1;
+    std::vector<int32_t> list, posv((size_t)x->n, -1);
+    for (int64_t j = 0; j < x->n; ++j) {
+        if (basic[(size_t)j] || !owns_col(x->P, j)) continue;
+        posv[(size_t)j] = (int32_t)list.size();
+        list.push_back((int32_t)j);
+    }
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    if (!list.empty())
+        HIP_TRY(hipMemcpy(x->P.nb_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(x->P.nb_pos, posv.data(), posv.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    SPX_TRY(read_state(x));
+    DevState st = *x->st_host;
+    st.status = ST_RUNNING;
+    st.nb_count = (int32_t)list.size();
+    st.p = -1;
+    st.min_e = 0.0;
+    HIP_TRY(hipMemcpy(x->P.st, &st, sizeof(st), hipMemcpyHostToDevice));
+    x->broken = true;  // until the inverse is rebuilt
+    SPX_TRY(reinvert_basis(x, basis));
+    x->broken = false;
+    x->refactor_base = x->pivots;
+    return SPX_OK;
 }
 
 int spx_iterate(spx_ctx* x, int64_t k, int32_t* status, int64_t* pivots) {

@@ -180,7 +180,25 @@ struct Params {
     double* Urows;  // KW x KW
     double* SY;     // KW
     double* xw;     // B_w b (L): r_tau . b = xw[q_tau] + sum_{s<tau} U[q_tau][s] Wt[n][s]
+    // leaving-row rule (include/simplex.h SPX_RATIO_*): candidates alpha_i >
+    // piv_tol (0 for the reference rule); GUARDED/HARRIS clamp x_b_i at 0
+    int32_t ratio;
+    int32_t pad_r;
+    double piv_tol;
+    double feas_tol;
 };
+
+enum : int32_t { RATIO_REFERENCE = 0, RATIO_GUARDED = 1, RATIO_HARRIS = 2 };
+
+// Ratio-test key of one row (compute_theta, v4:199-208, and the SPX_RATIO_*
+// variants); INFINITY when the row is not a candidate.  HARRIS returns the
+// first-pass key (max(x_b,0) + feas_tol) / alpha.
+__host__ __device__ inline double ratio_key(const Params& P, double xb, double a) {
+    if (!(a > P.piv_tol)) return INFINITY;
+    if (P.ratio == RATIO_REFERENCE) return xb / a;
+    const double xc = xb > 0.0 ? xb : 0.0;
+    return P.ratio == RATIO_HARRIS ? (xc + P.feas_tol) / a : xc / a;
+}
 
 __host__ __device__ inline bool owns_col(const Params& P, int64_t j) {
     return (j < P.ns) ? (j >= P.s_lo && j < P.s_hi) : (j >= P.k_lo && j < P.k_hi);

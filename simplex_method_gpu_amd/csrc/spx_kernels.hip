@@ -28,6 +28,7 @@
 #include <math.h>
 
 #include "spx_device.h"
+#include "spx_fold.h"
 #include "spx_kernels.h"
 
 namespace spx {
@@ -845,8 +846,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 a_new[i] = a;  // read back by the next pass (own row) / k_flush
                 if (upd_x) P.x_b[i] = xb;
             }
-            const bool pos = a > 0.0;
-            const double th = pos ? xb / a : INFINITY;
+            const bool pos = a > P.piv_tol;  // 0 for the reference rule (v4:202)
+            const double th = ratio_key(P, xb, a);
             wp.nonpos += !pos;
             wp.T = fma(cb, a, wp.T);
             if (argmin_better(th, i, wp.theta, wp.idx)) {
@@ -940,6 +941,58 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
     }
 }
 
+// Harris ratio test, second pass (SPX_RATIO_HARRIS; runs in k_tail, after
+// the k_update boundary made every row's alpha and updated x_b visible).  The
+// partials carry theta_max = min (max(x_b,0) + feas_tol) / alpha_i, the
+// nonpos count and T; the leaving row is the largest alpha_i among rows with
+// max(x_b_i,0) / alpha_i <= theta_max, first index on ties (the same rule as
+// oracle/simplex_oracle.c ratio_harris).
+template <int BLOCK>
+__device__ void harris_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
+                            unsigned char* smem, int nparts) {
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
+    if (t.nonpos == P.m || t.idx < 0 || t.idx >= P.m) {
+        if (tid == 0) {  // Unbounded (v4:319-322), as update_tail
+            st->p = p;
+            st->min_e = min_e;
+            st->status = ST_UNBOUNDED;
+        }
+        return;
+    }
+    const double thmax = t.theta;
+    const double* a_new = (it & 1) ? P.alpha0 : P.alpha1;
+    double bv = INFINITY;  // -alpha of the best candidate
+    int64_t bi = INT64_MAX;
+    for (int64_t i = tid; i < P.m; i += BLOCK) {
+        const double a = a_new[i];
+        if (a > P.piv_tol) {
+            const double xb = P.x_b[i];
+            const double xc = xb > 0.0 ? xb : 0.0;
+            if (xc / a <= thmax && argmin_better(-a, i, bv, bi)) { bv = -a; bi = i; }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double v = __shfl_xor(bv, off, 64);
+        const int64_t i = __shfl_xor(bi, off, 64);
+        if (argmin_better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+    __syncthreads();
+    ArgMinEntry* wr = reinterpret_cast<ArgMinEntry*>(red);  // reuse the partial slots
+    if (lane == 0) wr[wave] = ArgMinEntry{bv, bi};
+    __syncthreads();
+    if (tid != 0) return;
+    ArgMinEntry w = wr[0];
+    for (int k = 1; k < WAVES; ++k)
+        if (argmin_better(wr[k].val, wr[k].idx, w.val, w.idx)) w = wr[k];
+    const int64_t q = w.idx;  // exists: pass 1's winner satisfies the bound
+    const double aq = a_new[q], cbq = P.c_B[q];
+    pivot_bookkeeping(P, st, p, q, P.b_ixs[q], aq, y_scalar(t.T, aq, cbq, P.c[p]), min_e, it);
+}
+
 // The pivot tail as its own one-workgroup launch (split_tail): the k_update
 // workgroups stored their partials plainly and returned; the kernel boundary
 // makes them visible here.
@@ -956,6 +1009,8 @@ __global__ __launch_bounds__(1024) void k_tail(Params P, int nparts) {
     const int64_t it = st->iter;
     if (P.row_shard)
         update_tail_rs<1024>(P, st, it, (int)(it & 1), (it & 1) ? P.alpha1 : P.alpha0, smem, nparts);
+    else if (P.ratio == RATIO_HARRIS)
+        harris_tail<1024>(P, st, p, min_e, it, smem, nparts);
     else
         update_tail<1024>(P, st, p, min_e, it, smem, nparts);
 }
@@ -1014,15 +1069,12 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
 // operand, R the B operand.  B is read and written once.  min_nw: fold only
 // when nw >= min_nw (the loop asks for KW, a readback for 2).
 // ---------------------------------------------------------------------------
-typedef double dbl4 __attribute__((ext_vector_type(4)));
-
 template <int KW>
 __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
     DevState* st = P.st;
     const int nw = st->nw;
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
-    constexpr int KS = KW / 4;
     __shared__ double Rl[KW][64];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1031,17 +1083,7 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
     const int64_t c0 = (int64_t)blockIdx.x * 64;
     if (wave == 0) {
         double R[KW];
-#pragma unroll
-        for (int t = 0; t < KW; ++t) {
-            double v = 0.0;
-            if (t < nf) {
-                v = P.Qrows[(int64_t)t * L + c0 + lane];
-#pragma unroll
-                for (int s2 = 0; s2 < t; ++s2) v = fma(P.Urows[t * KW + s2], R[s2], v);
-            }
-            R[t] = v;
-            Rl[t][lane] = v;
-        }
+        fold_rebuild_R<KW>(P.Qrows, P.Urows, nf, L, c0, Rl, R);
         if (blockIdx.y == 0) {
             double* y = st->y_buf ? P.y1 : P.y0;
             double d = 0.0;
@@ -1052,53 +1094,11 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
         }
     }
     __syncthreads();
-    // R fragments (B operand): lane holds R[4s + (lane>>4)][16 jb + (lane&15)]
-    const int kr = lane >> 4, cl = lane & 15;
-    double bf[KS][4];
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) bf[s2][jb] = Rl[4 * s2 + kr][16 * jb + cl];
-    const int ks = (nf + 3) / 4;
     const int64_t m = P.m;
     const int64_t per = ((m + gridDim.y - 1) / gridDim.y + 15) / 16 * 16;
     const int64_t i0 = (int64_t)blockIdx.y * per;
     const int64_t i1 = (i0 + per < m) ? i0 + per : m;
-    double* B = P.B0;
-    for (int64_t r0 = i0 + 16 * wave; r0 < i1; r0 += 64) {
-        // U fragment (A operand): lane holds U[r0 + (lane&15)][4s + (lane>>4)]
-        const int64_t ia = r0 + cl;
-        double af[KS];
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            const int t = 4 * s2 + kr;
-            af[s2] = (ia < i1 && t < nf) ? P.U[ia * KW + t] : 0.0;
-        }
-        // B tile as the accumulator: lane holds rows r0 + kr + 4 r, column 16 jb + cl
-        dbl4 acc[4];
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t i = r0 + kr + 4 * r;
-                acc[jb][r] = (i < i1) ? B[i * L + c0 + 16 * jb + cl] : 0.0;
-            }
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            if (s2 < ks) {
-#pragma unroll
-                for (int jb = 0; jb < 4; ++jb)
-                    acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], bf[s2][jb], acc[jb], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t i = r0 + kr + 4 * r;
-                if (i < i1) B[i * L + c0 + 16 * jb + cl] = acc[jb][r];
-            }
-    }
+    fold_tiles<KW>(P.B0, P.U, nf, L, c0, i0, i1, Rl);
     if (blockIdx.x == 0) {  // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf)
         const double* wb = P.Wt + P.n * KW;
         for (int64_t i = i0 + tid; i < i1; i += 256) {

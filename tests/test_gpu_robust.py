@@ -1,0 +1,187 @@
+"""GPU: numerical-robustness options through the C-ABI,
+against the CPU oracle (oracle/simplex_oracle.c: ratio_test, orc_reinvert)
+and HiGHS optima computed here (tests/lpgen.py; an independent solver standing
+in for GLPK, solver_glpk.cpp:23).
+
+* leaving-row rules (spx_opts.ratio_test): on dense random LPs every rule
+  follows the oracle's pivot path exactly; on degenerate small-integer LPs
+  (tests/lpgen.py) the reference rule (v4:199-208) fails — it cycles or runs
+  x_b far negative — while GUARDED and HARRIS reach the HiGHS optimum within
+  1e-9 relative with x_b >= -1e-9.
+* reinversion (spx_reinvert): B^-1, x_b, y within 1e-10 relative of the
+  oracle's pivot-in reinversion of the same basis, and of the incrementally
+  updated state; the basis order is kept; periodic refactoring
+  (refactor_every) keeps the oracle's pivot path.
+* warm start (spx_set_basis): from an optimal basis the solve stops at once
+  with the same optimum; from a mid-solve basis it finishes at the optimum;
+  singular and malformed bases are refused.
+"""
+import numpy as np
+import pytest
+
+from lpgen import degenerate_lp, highs_opt
+
+pytestmark = pytest.mark.gpu
+
+RULES = [0, 1, 2]
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+@pytest.mark.parametrize("window", [-1, 64])
+@pytest.mark.parametrize("rule", RULES)
+@pytest.mark.parametrize("m,n,seed", [(64, 256, 0), (257, 771, 2)])
+def test_rules_follow_oracle_path(spx, oracle, rule, window, m, n, seed):
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, eps=1e-7, ratio=rule)
+    with spx.Context(A, b, c, eps=1e-7, ratio_test=rule, window=window) as ctx:
+        r = ctx.solve()
+    assert int(r.status) == ref.status == 1
+    assert r.pivots == ref.pivots
+    assert list(r.b_ixs) == list(ref.b_ixs)
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+    assert _rel(r.x_b, ref.x_b) <= 1e-9
+
+
+@pytest.mark.parametrize("window", [-1, 16])
+@pytest.mark.parametrize("m,n,seed", [(96, 300, 1), (128, 512, 2), (300, 900, 4)])
+def test_degenerate_lp_rules(spx, oracle, window, m, n, seed):
+    A, b, c = degenerate_lp(m, n, seed)
+    z_star = highs_opt(A, b, c)
+    cap = 20 * n
+    with spx.Context(A, b, c, eps=1e-7, window=window) as ctx:  # reference rule
+        r0 = ctx.solve(max_iter=cap)
+    assert not (r0.status == spx.SolveStatus.OptimumFound and abs(r0.z - z_star) <= 1e-6 * abs(z_star)
+                and r0.x_b.min() >= -1e-9)
+    for rule in (1, 2):
+        ref = oracle.solve(A, b, c, eps=1e-7, ratio=rule, max_iter=cap)
+        assert ref.status == 1 and abs(ref.z - z_star) <= 1e-9 * abs(z_star)
+        with spx.Context(A, b, c, eps=1e-7, ratio_test=rule, window=window) as ctx:
+            r = ctx.solve(max_iter=cap)
+        assert r.status == spx.SolveStatus.OptimumFound, rule
+        assert abs(r.z - z_star) <= 1e-9 * abs(z_star), (rule, r.z, z_star)
+        assert r.x_b.min() >= -1e-9, rule
+
+
+@pytest.mark.parametrize("window", [-1, 64])
+@pytest.mark.parametrize("m,n,seed,k", [(100, 300, 1, 70), (257, 771, 2, 200), (700, 2100, 3, 300)])
+def test_reinvert_matches_oracle(spx, oracle, window, m, n, seed, k):
+    A, b, c = oracle.generate(m, n, seed)
+    with spx.Context(A, b, c, eps=1e-7, window=window) as ctx:
+        st, piv = ctx.iterate(k)
+        before = ctx.state(binv=True)
+        ctx.reinvert()
+        after = ctx.state(binv=True)
+        e = ctx.reduced_costs()
+    assert list(after["b_ixs"]) == list(before["b_ixs"])
+    Bi, xb, y = oracle.reinvert(A, b, c, after["b_ixs"])
+    assert _rel(after["binv"], Bi) <= 1e-10
+    assert _rel(after["x_b"], xb) <= 1e-10
+    assert _rel(after["y"], y) <= 1e-10
+    assert _rel(after["binv"], before["binv"]) <= 1e-9
+    assert _rel(after["x_b"], before["x_b"]) <= 1e-9
+    assert _rel(e, oracle.price(A, c, after["y"])) <= 1e-12
+    Bmat = A[after["b_ixs"]].T
+    assert _rel(after["binv"] @ Bmat, np.eye(m)) <= 1e-10
+
+
+@pytest.mark.parametrize("window", [-1, 64])
+def test_reinvert_then_continue(spx, oracle, golden, window):
+    case = next(cs for cs in golden["cases"] if cs["m"] == 256)
+    m, n, seed = case["m"], case["n"], case["seed"]
+    with spx.Context(m=m, n=n, seed=seed, eps=1e-7, window=window) as ctx:
+        ctx.iterate(100)
+        ctx.reinvert()
+        r = ctx.solve()
+    assert r.status == spx.SolveStatus.OptimumFound
+    assert abs(r.z - case["highs_z"]) <= 1e-9 * abs(case["highs_z"])
+    assert sorted(int(j) for j in r.b_ixs) == case["highs_basis"]
+    assert r.pivots == case["oracle_pivots"]
+
+
+@pytest.mark.parametrize("window", [-1, 32])
+@pytest.mark.parametrize("K", [25, 64])
+def test_refactor_every_keeps_path(spx, oracle, window, K):
+    A, b, c = oracle.generate(200, 600, 7)
+    ref = oracle.solve(A, b, c, eps=1e-7, refactor_every=K, want_state=True)
+    with spx.Context(A, b, c, eps=1e-7, window=window, refactor_every=K) as ctx:
+        r = ctx.solve()
+        s = ctx.state(binv=True)
+    assert int(r.status) == ref.status == 1
+    assert r.pivots == ref.pivots
+    assert list(r.b_ixs) == list(ref.b_ixs)
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+    assert _rel(s["binv"], ref.binv) <= 1e-9
+    assert _rel(s["y"], ref.y) <= 1e-9
+
+
+@pytest.mark.parametrize("window", [-1, 64])
+def test_set_basis_warm_start(spx, oracle, window):
+    m, n, seed = 200, 800, 3
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, eps=1e-7, trace_cap=0)
+    mid = oracle.solve(A, b, c, eps=1e-7, max_iter=ref.pivots // 2)
+    with spx.Context(A, b, c, eps=1e-7, window=window) as ctx:
+        ctx.set_basis(ref.b_ixs)  # optimal basis: nothing to do
+        r = ctx.solve()
+        assert r.status == spx.SolveStatus.OptimumFound and r.pivots == 0
+        assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+        assert list(r.b_ixs) == list(ref.b_ixs)
+        ctx.set_basis(mid.b_ixs)  # mid-solve basis, reversed order
+        ctx.set_basis(mid.b_ixs[::-1].copy())
+        s = ctx.state()
+        assert _rel(s["x_b"], mid.x_b[::-1]) <= 1e-9
+        r = ctx.solve()
+    assert r.status == spx.SolveStatus.OptimumFound
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+    assert sorted(r.b_ixs) == sorted(ref.b_ixs)
+
+
+def test_set_basis_refuses_bad_bases(spx, oracle):
+    m, n = 50, 150
+    A, b, c = oracle.generate(m, n, 0)
+    A[1] = A[0]  # structural columns 0 and 1 identical
+    with spx.Context(A, b, c, eps=1e-7) as ctx:
+        basis = np.arange(n - m, n)
+        bad = basis.copy()
+        bad[3] = bad[4]
+        with pytest.raises(spx.SimplexError) as ei:
+            ctx.set_basis(bad)
+        assert ei.value.code == -1
+        sing = basis.copy()
+        sing[5], sing[9] = 0, 1
+        with pytest.raises(spx.SimplexError) as ei:
+            ctx.set_basis(sing)
+        assert ei.value.code == -7
+        with pytest.raises(spx.SimplexError):
+            ctx.iterate(1)  # no valid basis until reset
+        ctx.reset()
+        r = ctx.solve()
+    assert r.status == spx.SolveStatus.OptimumFound
+    with pytest.raises(ValueError):
+        oracle.reinvert(A, b, c, sing)
+
+
+def test_reinvert_c3_invariants(spx, oracle):
+    """C3 size (m=4096, n=16384): reinversion after 300 pivots against the
+    incremental state and B^-1 B = I on sampled basis columns."""
+    m, n, seed = 4096, 16384, 0
+    with spx.Context(m=m, n=n, seed=seed, eps=1e-7) as ctx:
+        ctx.iterate(300)
+        before = ctx.state(binv=True)
+        ctx.reinvert()
+        after = ctx.state(binv=True)
+    assert list(after["b_ixs"]) == list(before["b_ixs"])
+    assert _rel(after["binv"], before["binv"]) <= 1e-9
+    assert _rel(after["x_b"], before["x_b"]) <= 1e-9
+    assert _rel(after["y"], before["y"]) <= 1e-9
+    rng = np.random.default_rng(0)
+    for k in rng.choice(m, size=24, replace=False):
+        col = oracle.column_np(m, n, seed, int(after["b_ixs"][k]))
+        e = after["binv"] @ col
+        want = np.zeros(m)
+        want[k] = 1.0
+        assert np.max(np.abs(e - want)) <= 1e-10

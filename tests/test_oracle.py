@@ -110,3 +110,70 @@ def test_reader_rejects_m_gt_n(oracle, tmp_path):
     p.write_text("3 2\n1 2\n3 4\n5 6\n1 1 1\n1 1\n")
     with pytest.raises(ValueError):
         oracle.read_lp_text(str(p))
+
+
+# ---------------------------------------------------------------- §8f row 4
+def test_ratio_rules_agree_on_nondegenerate(oracle):
+    A, b, c = oracle.generate(128, 512, 0)
+    ref = oracle.solve(A, b, c, trace_cap=400)
+    for rule in (oracle.RATIO_GUARDED, oracle.RATIO_HARRIS):
+        r = oracle.solve(A, b, c, ratio=rule, trace_cap=400)
+        assert r.pivots == ref.pivots and list(r.b_ixs) == list(ref.b_ixs)
+        assert np.array_equal(r.trace_q, ref.trace_q)
+
+
+@pytest.mark.parametrize("m,n,seed", [(96, 300, 1), (128, 512, 2), (300, 900, 4)])
+def test_ratio_rules_on_degenerate_lps(oracle, m, n, seed):
+    """The reference rule (v4:199-208: no pivot guard, no x_b >= 0 filter)
+    loses feasibility on these degenerate LPs; the guarded and Harris rules
+    reach the HiGHS optimum."""
+    from lpgen import degenerate_lp, highs_opt
+
+    A, b, c = degenerate_lp(m, n, seed)
+    z_star = highs_opt(A, b, c)
+    cap = 20 * n
+    r0 = oracle.solve(A, b, c, max_iter=cap)
+    assert not (r0.status == oracle.OPTIMUM_FOUND and abs(r0.z - z_star) <= 1e-6 * abs(z_star))
+    for rule in (oracle.RATIO_GUARDED, oracle.RATIO_HARRIS):
+        r = oracle.solve(A, b, c, ratio=rule, max_iter=cap)
+        assert r.status == oracle.OPTIMUM_FOUND
+        assert abs(r.z - z_star) <= 1e-9 * abs(z_star)
+        assert r.x_b.min() >= -1e-9
+
+
+def test_reinvert_matches_numpy_inverse(oracle):
+    A, b, c = oracle.generate(120, 400, 5)
+    r = oracle.solve(A, b, c, max_iter=90, want_state=True)
+    Bi, xb, y = oracle.reinvert(A, b, c, r.b_ixs)
+    B = A[r.b_ixs].T
+    ref = np.linalg.inv(B)
+    assert np.max(np.abs(Bi - ref)) <= 1e-11 * max(1.0, np.max(np.abs(ref)))
+    assert np.allclose(xb, ref @ b, rtol=1e-11, atol=1e-11)
+    assert np.allclose(y, c[r.b_ixs] @ ref, rtol=1e-11, atol=1e-11)
+    assert np.max(np.abs(Bi - r.binv)) <= 1e-11 * max(1.0, np.max(np.abs(ref)))
+
+
+def test_reinvert_rejects_bad_bases(oracle):
+    m, n = 30, 90
+    A, b, c = oracle.generate(m, n, 0)
+    basis = np.arange(n - m, n)
+    dup = basis.copy()
+    dup[0] = dup[1]
+    with pytest.raises(ValueError, match="bad basis"):
+        oracle.reinvert(A, b, c, dup)
+    A2 = A.copy()
+    A2[1] = A2[0]
+    sing = basis.copy()
+    sing[2], sing[7] = 0, 1
+    with pytest.raises(ValueError, match="singular"):
+        oracle.reinvert(A2, b, c, sing)
+    Bi, xb, y = oracle.reinvert(A, b, c, basis)  # the slack basis: identity
+    assert np.array_equal(Bi, np.eye(m)) and np.array_equal(xb, b)
+
+
+def test_refactor_every_keeps_path(oracle):
+    A, b, c = oracle.generate(150, 450, 3)
+    ref = oracle.solve(A, b, c, trace_cap=1000)
+    r = oracle.solve(A, b, c, refactor_every=20, trace_cap=1000)
+    assert r.pivots == ref.pivots and np.array_equal(r.trace_q, ref.trace_q)
+    assert abs(r.z - ref.z) <= 1e-11 * abs(ref.z)
