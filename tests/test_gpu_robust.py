@@ -5,9 +5,9 @@ in for GLPK, solver_glpk.cpp:23).
 
 * leaving-row rules (spx_opts.ratio_test): on dense random LPs every rule
   follows the oracle's pivot path exactly; on degenerate small-integer LPs
-  (tests/lpgen.py) the reference rule (v4:199-208) fails — it cycles or runs
-  x_b far negative — while GUARDED and HARRIS reach the HiGHS optimum within
-  1e-9 relative with x_b >= -1e-9.
+  (tests/lpgen.py), where the oracle's reference rule (v4:199-208) cycles or
+  runs x_b far negative (tests/test_oracle.py), GUARDED and HARRIS reach the
+  HiGHS optimum within 1e-9 relative with x_b >= -1e-9.
 * reinversion (spx_reinvert): B^-1, x_b, y within 1e-10 relative of the
   oracle's pivot-in reinversion of the same basis, and of the incrementally
   updated state; the basis order is kept; periodic refactoring
@@ -52,10 +52,8 @@ def test_degenerate_lp_rules(spx, oracle, window, m, n, seed):
     A, b, c = degenerate_lp(m, n, seed)
     z_star = highs_opt(A, b, c)
     cap = 20 * n
-    with spx.Context(A, b, c, eps=1e-7, window=window) as ctx:  # reference rule
-        r0 = ctx.solve(max_iter=cap)
-    assert not (r0.status == spx.SolveStatus.OptimumFound and abs(r0.z - z_star) <= 1e-6 * abs(z_star)
-                and r0.x_b.min() >= -1e-9)
+    # (the reference rule's failure on these LPs is rounding-dependent; it is
+    # asserted on the deterministic oracle in test_oracle.py)
     for rule in (1, 2):
         ref = oracle.solve(A, b, c, eps=1e-7, ratio=rule, max_iter=cap)
         assert ref.status == 1 and abs(ref.z - z_star) <= 1e-9 * abs(z_star)
