@@ -12,8 +12,9 @@ LDFLAGS   := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl
 
 LIB       := $(PKG)/libsimplex.so
 CLI       := solver
+GLPKDRV   := solver_glpk
 
-all: $(LIB) $(CLI) oracle
+all: $(LIB) $(CLI) $(GLPKDRV) oracle
 
 $(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_device.h $(SRC)/spx_fold.h
 	@mkdir -p $(BUILD)
@@ -30,14 +31,18 @@ $(BUILD)/spx_api.o: $(SRC)/spx_api.cpp $(SRC)/spx_kernels.h $(SRC)/spx_reinv.h $
 $(LIB): $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDFLAGS)
 
-$(CLI): $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp $(SRC)/lp_io.h include/simplex.h $(LIB)
-	g++ -O2 -std=c++17 -Wall -pthread -Iinclude -o $@ $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp -L$(PKG) -Wl,-rpath,'$$ORIGIN/$(PKG)' -lsimplex
+$(CLI): $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp $(SRC)/lp_io.h $(SRC)/mps_io.cpp $(SRC)/mps_io.h include/simplex.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -pthread -Iinclude -o $@ $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp $(SRC)/mps_io.cpp -L$(PKG) -Wl,-rpath,'$$ORIGIN/$(PKG)' -lsimplex
+
+# GLPK CPU-baseline counterpart (solver_glpk.cpp): libglpk bound at run time
+$(GLPKDRV): $(SRC)/glpk_driver.cpp $(SRC)/lp_io.cpp $(SRC)/lp_io.h
+	g++ -O2 -std=c++17 -Wall -pthread -o $@ $(SRC)/glpk_driver.cpp $(SRC)/lp_io.cpp -ldl
 
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(CLI)
+	rm -rf $(BUILD) $(LIB) $(CLI) $(GLPKDRV)
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle

@@ -245,7 +245,7 @@ int write_binary(const std::string& path, const LP& lp, std::string& err) {
     return 0;
 }
 
-int write_text(const std::string& path, const LP& lp, std::string& err) {
+int write_text(const std::string& path, const LP& lp, std::string& err, const std::string& trailer) {
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) {
         err = "Could not open " + path + " for writing.";
@@ -258,6 +258,7 @@ int write_text(const std::string& path, const LP& lp, std::string& err) {
     }
     for (int64_t i = 0; i < lp.m; ++i) std::fprintf(f, i + 1 < lp.m ? "%.17g " : "%.17g\n", lp.b[(size_t)i]);
     for (int64_t j = 0; j < lp.n; ++j) std::fprintf(f, j + 1 < lp.n ? "%.17g " : "%.17g\n", lp.c[(size_t)j]);
+    if (!trailer.empty()) std::fputs(trailer.c_str(), f);
     if (std::fclose(f) != 0) {
         err = "write failed: " + path;
         return 1;

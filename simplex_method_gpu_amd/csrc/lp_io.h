@@ -29,7 +29,8 @@ int read_any(const std::string& path, LP& lp, std::string& err, int threads = 0)
 int read_text(const std::string& path, LP& lp, std::string& err, int threads = 0);
 int read_binary(const std::string& path, LP& lp, std::string& err);
 int write_binary(const std::string& path, const LP& lp, std::string& err);
-int write_text(const std::string& path, const LP& lp, std::string& err);
+// trailer: text appended after c (the reference's reader ignores it, v4:94-104)
+int write_text(const std::string& path, const LP& lp, std::string& err, const std::string& trailer = "");
 bool is_binary(const std::string& path);
 
 // Host copy of the seeded LP of SURVEY.md §8(d), bit-identical to the device

@@ -18,8 +18,24 @@
 //   --write-bin F  write the loaded/generated LP as binary .spxlp (lp_io.h)
 //   --write-text F write it in the reference's text format (%.17g, exact)
 //   --no-solve     stop after reading/writing
+//   --ratio R      leaving-row rule: reference | guarded | harris (simplex.h
+//                  SPX_RATIO_*; default reference, guarded with --mps)
+//   --piv-tol T, --feas-tol T   tolerances of the guarded / Harris rules
+//   --refactor K   rebuild B^-1 from the basis every K pivots (spx_reinvert)
+//   --window W     B^-1 representation (0 auto, -1 explicit, 8..64 eta window)
+//   --mps          the input is an MPS file (mps_io.h): converted to the
+//                  canonical form (slacks, senses, bounds, big-M artificials)
+//                  and solved; output as the reference's GLPK driver
+//                  (solver_glpk.cpp:27-38: "x[i] = v" per original column,
+//                  "Optimal objective: z", else "Problem status: <GLPK code>");
+//                  --write-text then writes the converted LP (the fixed
+//                  glpk_interface.cpp:80-98) with its recovery map as
+//                  trailing comment lines
+//   --big-m M      artificial cost (default 1e6 * max(1, max |c_j|))
 // The input file may be text or binary; binary is detected by its magic.
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +48,7 @@
 
 #include "../../include/simplex.h"
 #include "lp_io.h"
+#include "mps_io.h"
 
 using Clock = std::chrono::steady_clock;
 using TimePoint = Clock::time_point;
@@ -47,7 +64,9 @@ static void print_elapsed_time(const char* msg, double dur) {
 
 static void usage() {
     std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
-                 " [--threads T] [--write-bin F] [--write-text F] [--no-solve] (<file> | --gen m n seed)\n";
+                 " [--threads T] [--write-bin F] [--write-text F] [--no-solve] [--ratio reference|guarded|harris]"
+                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--mps [--big-m M]]"
+                 " (<file> | --gen m n seed)\n";
 }
 
 int main(int argc, char* argv[]) {
@@ -61,6 +80,10 @@ int main(int argc, char* argv[]) {
     int64_t gm = 0, gn = 0;
     uint64_t gseed = 0;
     const char* path = nullptr;
+    int ratio = -1, window = 0;
+    double piv_tol = 1e-9, feas_tol = 1e-9, big_m = 0.0;
+    int64_t refactor = 0;
+    bool mps_in = false;
     for (int a = 1; a < argc; ++a) {
         const std::string s = argv[a];
         auto need = [&](int k) {
@@ -79,6 +102,21 @@ int main(int argc, char* argv[]) {
         else if (s == "--write-bin") { need(1); write_bin = argv[++a]; }
         else if (s == "--write-text") { need(1); write_text = argv[++a]; }
         else if (s == "--no-solve") solve = false;
+        else if (s == "--ratio") {
+            need(1);
+            const std::string r = argv[++a];
+            ratio = r == "reference" ? SPX_RATIO_REFERENCE
+                  : r == "guarded"   ? SPX_RATIO_GUARDED
+                  : r == "harris"    ? SPX_RATIO_HARRIS
+                                     : -2;
+            if (ratio == -2) { usage(); return 1; }
+        }
+        else if (s == "--piv-tol") { need(1); piv_tol = std::strtod(argv[++a], nullptr); }
+        else if (s == "--feas-tol") { need(1); feas_tol = std::strtod(argv[++a], nullptr); }
+        else if (s == "--refactor") { need(1); refactor = std::strtoll(argv[++a], nullptr, 10); }
+        else if (s == "--window") { need(1); window = std::atoi(argv[++a]); }
+        else if (s == "--mps") mps_in = true;
+        else if (s == "--big-m") { need(1); big_m = std::strtod(argv[++a], nullptr); }
         else if (s == "--gen") {
             need(3);
             gen = true;
@@ -97,8 +135,17 @@ int main(int argc, char* argv[]) {
     const TimePoint t_start = Clock::now();
     TimePoint t_host_alloc = t_start, t_read = t_start, t_solve = t_start;
     lpio::LP lp;
-    std::string err;
-    if (!gen) {
+    mps::Problem pb;
+    std::string err, trailer;
+    if (mps_in && !gen) {
+        t_host_alloc = t_read = Clock::now();
+        if (mps::read_mps(path, pb, err, big_m) != 0) {
+            std::cerr << err << "\n";
+            return EXIT_FAILURE;
+        }
+        lp = std::move(pb.lp);
+        trailer = mps::map_block(pb);
+    } else if (!gen) {
         t_host_alloc = t_read = Clock::now();
         if (lpio::read_any(path, lp, err, threads) != 0) {
             std::cerr << err << "\n";
@@ -111,7 +158,7 @@ int main(int argc, char* argv[]) {
         if (!write_bin.empty() || !write_text.empty()) lpio::generate(gm, gn, gseed, lp);
     }
     if ((!write_bin.empty() && lpio::write_binary(write_bin, lp, err) != 0) ||
-        (!write_text.empty() && lpio::write_text(write_text, lp, err) != 0)) {
+        (!write_text.empty() && lpio::write_text(write_text, lp, err, trailer) != 0)) {
         std::cerr << err << "\n";
         return EXIT_FAILURE;
     }
@@ -126,6 +173,11 @@ int main(int argc, char* argv[]) {
     spx_default_opts(&o);
     o.eps = eps;
     o.device = device;
+    o.ratio_test = ratio >= 0 ? ratio : (mps_in ? SPX_RATIO_GUARDED : SPX_RATIO_REFERENCE);
+    o.piv_tol = piv_tol;
+    o.feas_tol = feas_tol;
+    o.refactor_every = (int32_t)refactor;
+    o.window = window;
     spx_ctx* ctx = nullptr;
     const TimePoint t_alloc = Clock::now();
     int rc = device_gen ? spx_create_generated(&ctx, m, n, gseed, &o)
@@ -147,6 +199,38 @@ int main(int argc, char* argv[]) {
     const TimePoint t_loop_end = Clock::now();
     spx_destroy(ctx);
     const TimePoint t_dealloc_end = Clock::now();
+
+    if (mps_in) {  // the reference's GLPK driver output (solver_glpk.cpp:27-38)
+        pb.lp.m = m;
+        pb.lp.n = n;
+        std::vector<double> xb(x_b.begin(), x_b.begin() + m);
+        std::vector<int64_t> bix(b_ixs.begin(), b_ixs.begin() + m);
+        const double art = mps::max_artificial(pb, xb, bix);
+        double bmax = 1.0;
+        for (double v : lp.b) bmax = std::max(bmax, std::fabs(v));
+        const bool feasible = art <= 1e-7 * bmax;
+        const std::vector<double> xs = mps::recover_x(pb, xb, bix);
+        const double zo = mps::objective(pb, xs);
+        // GLPK status codes: GLP_OPT 5, GLP_NOFEAS 4, GLP_UNBND 6, GLP_UNDEF 1
+        const int glp = status == SPX_STATUS_OPTIMUM_FOUND ? (feasible ? 5 : 4)
+                        : status == SPX_STATUS_UNBOUNDED   ? 6
+                                                           : 1;
+        if (glp == 5) {
+            for (size_t j = 0; j < xs.size(); ++j) std::cout << "x[" << j + 1 << "] = " << xs[j] << "\n";
+            std::cout << "Optimal objective: " << zo << "\n";
+        } else {
+            std::cout << "Problem status: " << glp << "\n";
+        }
+        if (json) {
+            std::cout << std::defaultfloat << std::setprecision(17);
+            std::cout << "{\"status\": " << status << ", \"glp_status\": " << glp << ", \"z\": " << zo
+                      << ", \"pivots\": " << pivots << ", \"m\": " << m << ", \"n\": " << n
+                      << ", \"max_artificial\": " << art << ", \"x\": [";
+            for (size_t j = 0; j < xs.size(); ++j) std::cout << (j ? ", " : "") << xs[j];
+            std::cout << "]}\n";
+        }
+        return 0;
+    }
 
     // "# Iteration k" once per loop pass (v4:287): pivots + the terminating pass
     const int64_t passes = (status == SPX_STATUS_MAX_ITER) ? pivots : pivots + 1;
