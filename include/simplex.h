@@ -88,8 +88,23 @@ typedef struct spx_opts {
                              piv_tol (default 1e-9)                           */
     double  feas_tol;     /* SPX_RATIO_HARRIS: primal feasibility tolerance
                              delta of the first pass (default 1e-9)          */
-    int32_t reserved[4];
+    int32_t pricing;      /* entering-column rule, SPX_PRICING_* (default DANTZIG) */
+    int32_t reserved[3];
 } spx_opts;
+
+/* Entering-column rules (README.md:16-17 "steepest edge").
+ * DANTZIG: most negative e_j (v4:288-302).
+ * DEVEX:   Devex reference weights w_j (1 at the start): after a pivot with
+ *          pivot element alpha_q, entering weight w_p and pivot row
+ *          alpha_rj = r.A_j (r = row q of B^-1 before the pivot),
+ *          w_j = max(w_j, (alpha_rj/alpha_q)^2 w_p) for non-basic j and
+ *          w_leave = max(w_p/alpha_q^2, 1); p = argmin of -e_j^2/w_j over
+ *          e_j < -eps (first index on ties).  The pivot row comes free from
+ *          the eta-window pricing pass (it computes r.A_j for every column),
+ *          so DEVEX needs the window (opts.window 0 selects 64) and one rank.
+ *          spx_price's min_e is then the entering column's reduced cost. */
+#define SPX_PRICING_DANTZIG 0
+#define SPX_PRICING_DEVEX   1
 
 /* Leaving-row rules.
  * REFERENCE: theta_i = x_b_i / alpha_i over alpha_i > 0, first index on ties

@@ -30,12 +30,14 @@ _lib = None
 
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
+# entering-column rules (include/simplex.h SPX_PRICING_*)
+PRICING_DANTZIG, PRICING_DEVEX = 0, 1
 
 
 class OrcOpts(ctypes.Structure):
     _fields_ = [("max_iter", ctypes.c_int64), ("eps", ctypes.c_double), ("threads", ctypes.c_int),
                 ("ratio", ctypes.c_int), ("piv_tol", ctypes.c_double), ("feas_tol", ctypes.c_double),
-                ("refactor_every", ctypes.c_int64)]
+                ("refactor_every", ctypes.c_int64), ("pricing", ctypes.c_int)]
 
 
 def build() -> str:
@@ -172,7 +174,7 @@ class OracleResult:
 def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 << 40,
           eps: float = 1e-7, threads: int = 0, trace_cap: int = 0,
           want_state: bool = False, ratio: int = RATIO_REFERENCE, piv_tol: float = 1e-9,
-          feas_tol: float = 1e-9, refactor_every: int = 0) -> OracleResult:
+          feas_tol: float = 1e-9, refactor_every: int = 0, pricing: int = 0) -> OracleResult:
     n, m = A_cols.shape
     A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
@@ -189,6 +191,7 @@ def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 <<
     lib().orc_default_opts(ctypes.byref(o))
     o.max_iter, o.eps, o.threads = max_iter, eps, threads
     o.ratio, o.piv_tol, o.feas_tol, o.refactor_every = ratio, piv_tol, feas_tol, refactor_every
+    o.pricing = pricing
     st = lib().orc_solve_ex(m, n, _ptr(A_cols), _ptr(b), _ptr(c), ctypes.byref(o),
                             ctypes.byref(z), _ptr(x_b), _ptr(b_ixs), ctypes.byref(piv),
                             _ptr(tp), _ptr(tq), trace_cap, _ptr(y), _ptr(binv))

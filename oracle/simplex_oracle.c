@@ -100,6 +100,13 @@ typedef struct {
     int64_t m, n;
     double *Binv, *c_b, *x_b, *y, *e, *alpha, *theta, *E, *r;
     int64_t* b_ixs;
+    /* Devex pricing (orc_opts.pricing = 1): reference weights, basic mask and
+     * the last pivot's data (r above is its pivot row of B^-1) */
+    double* w;
+    char* basic;
+    int dvx_pend;
+    double dvx_aq, dvx_wp;
+    int64_t dvx_leave;
 } orc_state;
 
 static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
@@ -116,9 +123,13 @@ static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
     s->E = (double*)malloc(sizeof(double) * (size_t)m);
     s->r = (double*)malloc(sizeof(double) * (size_t)m);
     s->b_ixs = (int64_t*)malloc(sizeof(int64_t) * (size_t)m);
+    s->w = (double*)malloc(sizeof(double) * (size_t)n);
+    s->basic = (char*)calloc((size_t)n, 1);
     if (!s->Binv || !s->c_b || !s->x_b || !s->y || !s->e || !s->alpha ||
-        !s->theta || !s->E || !s->r || !s->b_ixs)
+        !s->theta || !s->E || !s->r || !s->b_ixs || !s->w || !s->basic)
         return -1;
+    for (int64_t j = 0; j < n; ++j) s->w[j] = 1.0;
+    for (int64_t j = n - m; j < n; ++j) s->basic[j] = 1;
     /* init_I (v4:182-188, launch :272): B^-1 = I_m */
 #pragma omp parallel for schedule(static)
     for (int64_t k = 0; k < m; ++k)
@@ -135,6 +146,7 @@ static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
 static void state_free(orc_state* s) {
     free(s->Binv); free(s->c_b); free(s->x_b); free(s->y); free(s->e);
     free(s->alpha); free(s->theta); free(s->E); free(s->r); free(s->b_ixs);
+    free(s->w); free(s->basic);
 }
 
 /* One pass of the do-loop body (v4:286-357).  Returns ORC_MAX_ITER when a
@@ -180,16 +192,60 @@ static int64_t ratio_test(const orc_state* s, int rule, double piv_tol,
     return q;
 }
 
+/* Devex entering column (README.md:16-17 "steepest edge"; the reference
+ * framework of Forrest & Goldfarb's Devex).  First the weights of the
+ * non-basic columns take the last pivot into account: with alpha_rj = r.A_j
+ * its pivot-row entries (r = row q of B^-1 before that pivot), alpha_q its
+ * pivot and w_p the entering column's weight,
+ *   w_j = max(w_j, (alpha_rj / alpha_q)^2 w_p),  w_leave = max(w_p / alpha_q^2, 1).
+ * Then p = argmin over non-basic j with e_j < -eps of -(e_j^2) / w_j (first
+ * index on ties); -1 when there is none (optimal). */
+static int64_t devex_choose(orc_state* s, const double* A, double eps) {
+    const int64_t m = s->m, n = s->n;
+    if (s->dvx_pend) {
+        const double aq = s->dvx_aq, wp = s->dvx_wp;
+#pragma omp parallel for schedule(static)
+        for (int64_t j = 0; j < n; ++j) {
+            if (s->basic[j]) continue;
+            if (j == s->dvx_leave) {
+                const double v = wp / (aq * aq);
+                s->w[j] = v > 1.0 ? v : 1.0;
+                continue;
+            }
+            const double* col = A + j * m;
+            double a = 0.0;
+            for (int64_t k = 0; k < m; ++k) a += s->r[k] * col[k];
+            const double g = a / aq;
+            const double v = g * g * wp;
+            if (v > s->w[j]) s->w[j] = v;
+        }
+    }
+    int64_t p = -1;
+    double best = INFINITY;
+    for (int64_t j = 0; j < n; ++j) {
+        if (s->basic[j] || !(s->e[j] < -eps)) continue;
+        const double key = -(s->e[j] * s->e[j]) / s->w[j];
+        if (key < best) { best = key; p = j; }
+    }
+    return p;
+}
+
 static int one_pass(orc_state* s, const double* A, const double* b,
                     const double* c, double eps, int rule, double piv_tol,
-                    double feas_tol, int64_t* p_out, int64_t* q_out) {
+                    double feas_tol, int pricing, int64_t* p_out, int64_t* q_out) {
     const int64_t m = s->m, n = s->n;
     double min_val;
 
-    /* pricing GEMM + entering ArgMin (v4:289-302) */
+    /* pricing GEMM + entering ArgMin (v4:289-302), or Devex */
     orc_price(m, n, A, c, s->y, s->e, 0);
-    const int64_t p = argmin_first(s->e, n, &min_val);
-    if (min_val >= -eps) return ORC_OPTIMUM_FOUND;
+    int64_t p;
+    if (pricing == 1) {
+        p = devex_choose(s, A, eps);
+        if (p < 0) return ORC_OPTIMUM_FOUND;
+    } else {
+        p = argmin_first(s->e, n, &min_val);
+        if (min_val >= -eps) return ORC_OPTIMUM_FOUND;
+    }
 
     /* FTRAN: alpha = B_inv * A_p (cublasSgemv, v4:307-308) */
     const double* Ap = A + p * m;
@@ -228,6 +284,12 @@ static int one_pass(orc_state* s, const double* A, const double* b,
     /* basis bookkeeping (v4:339-342) */
     const double c_bq = s->c_b[q];
     const double c_p = c[p];
+    s->dvx_leave = s->b_ixs[q];
+    s->basic[s->dvx_leave] = 0;
+    s->basic[p] = 1;
+    s->dvx_pend = 1;
+    s->dvx_aq = aq;
+    s->dvx_wp = s->w[p];
     s->c_b[q] = c_p;
     s->b_ixs[q] = p;
 
@@ -360,6 +422,7 @@ void orc_default_opts(orc_opts* o) {
     o->piv_tol = 1e-9;
     o->feas_tol = 1e-9;
     o->refactor_every = 0;
+    o->pricing = 0;
 }
 
 int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
@@ -377,7 +440,7 @@ int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
     if (o->max_iter > 0) {
         do { /* v4:286-359 */
             int64_t p = -1, q = -1;
-            status = one_pass(&s, A, b, c, o->eps, o->ratio, o->piv_tol, o->feas_tol, &p, &q);
+            status = one_pass(&s, A, b, c, o->eps, o->ratio, o->piv_tol, o->feas_tol, o->pricing, &p, &q);
             if (status != ORC_MAX_ITER) break;
             if (i < trace_cap) {
                 if (trace_p) trace_p[i] = p;
@@ -432,7 +495,7 @@ double orc_time_iterations(int64_t m, int64_t n, const double* A,
     int64_t k = 0;
     for (; k < iters; ++k) {
         int64_t p, q;
-        if (one_pass(&s, A, b, c, -1.0e300, 0, 0.0, 0.0, &p, &q) != ORC_MAX_ITER) break;
+        if (one_pass(&s, A, b, c, -1.0e300, 0, 0.0, 0.0, 0, &p, &q) != ORC_MAX_ITER) break;
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     if (done) *done = k;

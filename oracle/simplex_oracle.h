@@ -74,6 +74,7 @@ typedef struct {
     double piv_tol;
     double feas_tol;
     int64_t refactor_every;
+    int pricing; /* 0 Dantzig (v4:288-302), 1 Devex (simplex_oracle.c devex_choose) */
 } orc_opts;
 
 void orc_default_opts(orc_opts* o);

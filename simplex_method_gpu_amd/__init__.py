@@ -24,7 +24,8 @@ from ._lib import SimplexError, SpxOpts, check, load
 
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
            "shard_range", "minloc_merge", "group_iterate", "group_sync",
-           "SimplexError", "FLAG_TIMING", "RATIO_REFERENCE", "RATIO_GUARDED", "RATIO_HARRIS"]
+           "SimplexError", "FLAG_TIMING", "RATIO_REFERENCE", "RATIO_GUARDED", "RATIO_HARRIS",
+           "PRICING_DANTZIG", "PRICING_DEVEX"]
 
 FLAG_TIMING = 1
 FLAG_STAMPS = 2
@@ -34,6 +35,8 @@ FLAG_SPLIT_TAIL = 16
 
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
+# entering-column rules (include/simplex.h SPX_PRICING_*)
+PRICING_DANTZIG, PRICING_DEVEX = 0, 1
 
 
 class SolveStatus(IntEnum):
@@ -122,7 +125,8 @@ class Context:
                  nranks: int = 1, graph_batch: int = 0, timing: bool = False, price_block: int = 0,
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
                  global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
-                 ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0):
+                 ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0,
+                 pricing: int = 0):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -132,6 +136,7 @@ class Context:
         o.window = window  # 0 auto, -1 explicit rank-1 B^-1 update, 8/16/32/64 eta window
         o.ratio_test, o.piv_tol, o.feas_tol = ratio_test, piv_tol, feas_tol  # RATIO_*
         o.refactor_every = refactor_every
+        o.pricing = pricing  # PRICING_DANTZIG / PRICING_DEVEX
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
                    | (FLAG_SPLIT_TAIL if split_tail else 0))

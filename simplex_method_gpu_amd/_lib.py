@@ -35,7 +35,8 @@ class SpxOpts(ctypes.Structure):
         ("refactor_every", ctypes.c_int32),
         ("piv_tol", ctypes.c_double),
         ("feas_tol", ctypes.c_double),
-        ("reserved", ctypes.c_int32 * 4),
+        ("pricing", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 

@@ -23,6 +23,7 @@
 //   --piv-tol T, --feas-tol T   tolerances of the guarded / Harris rules
 //   --refactor K   rebuild B^-1 from the basis every K pivots (spx_reinvert)
 //   --window W     B^-1 representation (0 auto, -1 explicit, 8..64 eta window)
+//   --pricing P    entering-column rule: dantzig (v4:288-302, default) | devex
 //   --mps          the input is an MPS file (mps_io.h): converted to the
 //                  canonical form (slacks, senses, bounds, big-M artificials)
 //                  and solved; output as the reference's GLPK driver
@@ -65,7 +66,8 @@ static void print_elapsed_time(const char* msg, double dur) {
 static void usage() {
     std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
                  " [--threads T] [--write-bin F] [--write-text F] [--no-solve] [--ratio reference|guarded|harris]"
-                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--mps [--big-m M]]"
+                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--pricing dantzig|devex]"
+                 " [--mps [--big-m M]]"
                  " (<file> | --gen m n seed)\n";
 }
 
@@ -80,7 +82,7 @@ int main(int argc, char* argv[]) {
     int64_t gm = 0, gn = 0;
     uint64_t gseed = 0;
     const char* path = nullptr;
-    int ratio = -1, window = 0;
+    int ratio = -1, window = 0, pricing = SPX_PRICING_DANTZIG;
     double piv_tol = 1e-9, feas_tol = 1e-9, big_m = 0.0;
     int64_t refactor = 0;
     bool mps_in = false;
@@ -116,6 +118,12 @@ int main(int argc, char* argv[]) {
         else if (s == "--refactor") { need(1); refactor = std::strtoll(argv[++a], nullptr, 10); }
         else if (s == "--window") { need(1); window = std::atoi(argv[++a]); }
         else if (s == "--mps") mps_in = true;
+        else if (s == "--pricing") {
+            need(1);
+            const std::string r = argv[++a];
+            pricing = r == "dantzig" ? SPX_PRICING_DANTZIG : r == "devex" ? SPX_PRICING_DEVEX : -1;
+            if (pricing < 0) { usage(); return 1; }
+        }
         else if (s == "--big-m") { need(1); big_m = std::strtod(argv[++a], nullptr); }
         else if (s == "--gen") {
             need(3);
@@ -178,6 +186,7 @@ int main(int argc, char* argv[]) {
     o.feas_tol = feas_tol;
     o.refactor_every = (int32_t)refactor;
     o.window = window;
+    o.pricing = pricing;
     spx_ctx* ctx = nullptr;
     const TimePoint t_alloc = Clock::now();
     int rc = device_gen ? spx_create_generated(&ctx, m, n, gseed, &o)

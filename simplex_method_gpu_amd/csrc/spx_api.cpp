@@ -162,6 +162,7 @@ void spx_default_opts(spx_opts* o) {
     o->refactor_every = 0;
     o->piv_tol = 1e-9;
     o->feas_tol = 1e-9;
+    o->pricing = SPX_PRICING_DANTZIG;
 }
 
 const char* spx_last_error(void) { return g_err.c_str(); }
@@ -280,6 +281,17 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         // latency-bound) stay explicit.  Row-sharded B^-1 is always explicit.
         const bool pays = m >= 2048 && (double)m >= 0.06 * (double)(n - m);
         KW = (pays && !P.row_shard) ? 64 : -1;
+    }
+    // Devex pricing takes the pivot row from the eta-window pricing pass
+    if (x->opts.pricing != SPX_PRICING_DANTZIG && x->opts.pricing != SPX_PRICING_DEVEX)
+        return fail(SPX_ERR_ARG, "bad pricing %d", x->opts.pricing);
+    P.devex = x->opts.pricing == SPX_PRICING_DEVEX ? 1 : 0;
+    if (P.devex) {
+        if (G > 1) return fail(SPX_ERR_ARG, "Devex pricing runs on one rank");
+        if (x->opts.window < 0) return fail(SPX_ERR_ARG, "Devex pricing needs the eta window (window > 0 or 0 = auto)");
+        if (x->opts.window == 0) KW = 64;
+        SPX_TRY(x->alloc(&P.W, (size_t)n));
+        SPX_TRY(x->alloc(&P.dvx_e, 1));
     }
     if (KW > 0 && P.row_shard) return fail(SPX_ERR_ARG, "the eta window needs replicated B^-1 (no row sharding)");
     if (KW > 0 && !(KW == 8 || KW == 16 || KW == 32 || KW == 64))
@@ -804,7 +816,13 @@ int spx_set_basis(spx_ctx* x, const int64_t* basis) {
     st.nb_count = (int32_t)list.size();
     st.p = -1;
     st.min_e = 0.0;
+    st.leave = -1;  // Devex: a fresh reference framework
+    st.wp = 1.0;
     HIP_TRY(hipMemcpy(x->P.st, &st, sizeof(st), hipMemcpyHostToDevice));
+    if (x->P.W) {
+        const std::vector<double> ones((size_t)x->n, 1.0);
+        HIP_TRY(hipMemcpy(x->P.W, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     x->broken = true;  // until the inverse is rebuilt
     SPX_TRY(reinvert_basis(x, basis));
     x->broken = false;
@@ -1028,8 +1046,10 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
         if (argmin_better(e.val, e.idx, best.val, best.idx)) best = e;
     }
     if (p) *p = (best.idx == INT64_MAX) ? -1 : best.idx;
-    if (min_e) *min_e = best.val;
-    if (optimal) *optimal = (best.val >= -x->opts.eps || best.idx == INT64_MAX) ? 1 : 0;
+    double e_enter = best.val;
+    if (x->P.devex) HIP_TRY(hipMemcpy(&e_enter, x->P.dvx_e, sizeof(double), hipMemcpyDeviceToHost));
+    if (min_e) *min_e = e_enter;
+    if (optimal) *optimal = no_entering(x->P, best.val, best.idx) ? 1 : 0;
     x->stepped_price = true;
     return SPX_OK;
 }

@@ -121,7 +121,9 @@ struct alignas(16) DevState {
     int32_t nw;          // eta window: pivots since the last fold (nw-1 pending)
     uint32_t ticket_fold;
     int32_t pad1;
-    int64_t pad2;
+    int64_t leave;       // Devex: column that left at the last pivot (-1 none)
+    double wp;           // Devex: weight of the last entering column
+    double pad3;
 };
 
 __host__ __device__ inline bool argmin_better(double v, int64_t j, double bv, int64_t bj) {
@@ -183,10 +185,19 @@ struct Params {
     // leaving-row rule (include/simplex.h SPX_RATIO_*): candidates alpha_i >
     // piv_tol (0 for the reference rule); GUARDED/HARRIS clamp x_b_i at 0
     int32_t ratio;
-    int32_t pad_r;
+    int32_t devex;         // SPX_PRICING_DEVEX (eta window, one rank)
     double piv_tol;
     double feas_tol;
+    double* W;             // Devex reference weights (n)
+    double* dvx_e;         // Devex: reduced cost of the chosen column (k_price -> k_update)
 };
+
+// Optimality test on the merged entering candidate (v4:299-302): the reduced
+// cost itself under Dantzig; under Devex the key -e^2/w is +inf exactly when
+// no e_j < -eps.
+__host__ __device__ inline bool no_entering(const Params& P, double val, int64_t p) {
+    return p == INT64_MAX || (P.devex ? !(val < INFINITY) : val >= -P.eps);
+}
 
 enum : int32_t { RATIO_REFERENCE = 0, RATIO_GUARDED = 1, RATIO_HARRIS = 2 };
 

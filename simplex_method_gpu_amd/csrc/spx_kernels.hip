@@ -286,8 +286,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
     }
 
-    double best = INFINITY, bw = 0.0;
+    double best = INFINITY, bw = 0.0, be = 0.0;
     int64_t bj = INT64_MAX;
+    const int64_t dvx_leave = st->leave;
+    const double dvx_wp = st->wp, dvx_aq = st->aq;
     unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
     const int nlist = nb;
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&cn[lane + u * 64]);
         }
-        double e, wn = 0.0;
+        double e, wn = 0.0, key;
         if (WIN && pend) {
             // r_tau . A_j = B_w[q,:] . A_j + sum_s U[q][s] Wt[j][s]; the window
             // terms join the lane partials before the butterflies
@@ -389,12 +391,27 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         } else {
             e = wave_sum(a0 + a1) - P.c[j];
         }
-        if (argmin_better(e, j, best, bj)) { best = e; bj = j; bw = wn; }
+        key = e;
+        if (WIN && P.devex) {
+            // Devex (include/simplex.h SPX_PRICING_DEVEX): the pending pivot's
+            // row entry wn = r.A_j updates this column's reference weight
+            double w = P.W[j];
+            if (pend) {
+                if (j == dvx_leave) w = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
+                else {
+                    const double g = wn / dvx_aq;
+                    w = fmax(w, g * g * dvx_wp);
+                }
+                if (lane == 0) P.W[j] = w;
+            }
+            key = (e < -P.eps) ? -(e * e) / w : INFINITY;
+        }
+        if (argmin_better(key, j, best, bj)) { best = key; bj = j; bw = wn; be = e; }
     }
 
     stamp_stream(win, false);
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
-    if (lane == 0) red[wave] = PricePartial{best, bj, bw, 0.0};
+    if (lane == 0) red[wave] = PricePartial{best, bj, bw, be};
     __syncthreads();
     if (tid == 0) {
         PricePartial w = red[0];
@@ -402,7 +419,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
         st_agent(&P.price_partials[blockIdx.x].val, w.val);
         st_agent(&P.price_partials[blockIdx.x].idx, w.idx);
-        if constexpr (WIN) st_agent(&P.price_partials[blockIdx.x].w, w.w);
+        if constexpr (WIN) {
+            st_agent(&P.price_partials[blockIdx.x].w, w.w);
+            st_agent(&P.price_partials[blockIdx.x].pad, w.pad);
+        }
         drain_vmem();
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_price, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -417,14 +437,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
         const double v = ld_agent(&P.price_partials[g].val);
         const int64_t i = ld_agent(&P.price_partials[g].idx);
-        if (argmin_better(v, i, w.val, w.idx)) w = PricePartial{v, i, WIN ? ld_agent(&P.price_partials[g].w) : 0.0, 0.0};
+        if (argmin_better(v, i, w.val, w.idx))
+            w = PricePartial{v, i, WIN ? ld_agent(&P.price_partials[g].w) : 0.0,
+                             WIN ? ld_agent(&P.price_partials[g].pad) : 0.0};
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const double v = __shfl_xor(w.val, off, 64);
         const int64_t i = __shfl_xor(w.idx, off, 64);
         const double ww = __shfl_xor(w.w, off, 64);
-        if (argmin_better(v, i, w.val, w.idx)) w = PricePartial{v, i, ww, 0.0};
+        const double we = __shfl_xor(w.pad, off, 64);
+        if (argmin_better(v, i, w.val, w.idx)) w = PricePartial{v, i, ww, we};
     }
     __syncthreads();
     if (lane == 0) red[wave] = w;
@@ -434,6 +457,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
     if (tid == 0) {
         P.price_out[0] = ArgMinEntry{t.val, t.idx};
+        if (WIN && P.devex) *P.dvx_e = t.pad;
         st_agent(&st->ticket_price, 0u);
     }
     if (WIN && P.nin > 1) {
@@ -581,9 +605,13 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
         st->y_applied = it;
     }
     st->xb_applied = it;
+    if (P.devex) {
+        st->leave = leave;
+        st->wp = P.W[p];
+    }
     st->p = p;
     st->q = q;
-    st->min_e = min_e;
+    st->min_e = P.devex ? *P.dvx_e : min_e;
     st->iter = it + 1;
 }
 
@@ -639,7 +667,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         const ArgMinEntry e = P.price_in[g * P.pr_stride];
         if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
     }
-    if (min_e >= -P.eps || p == INT64_MAX) {  // OptimumFound (v4:299-302)
+    if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
             st->min_e = min_e;
@@ -1263,6 +1291,7 @@ __global__ void k_reset(Params P) {
         if (P.xw) P.xw[i] = P.b[i];  // B_w = I
     }
     for (int64_t j = t0; j < n; j += stride) {
+        if (P.W) P.W[j] = 1.0;  // Devex reference framework
         int32_t pos = -1;
         if (j < ns && j >= P.s_lo && j < P.s_hi) {
             pos = (int32_t)(j - P.s_lo);
@@ -1289,6 +1318,8 @@ __global__ void k_reset(Params P) {
         st->ticket_update = 0;
         st->nw = 0;
         st->ticket_fold = 0;
+        st->leave = -1;
+        st->wp = 1.0;
     }
 }
 

@@ -183,3 +183,42 @@ def test_reinvert_c3_invariants(spx, oracle):
         want = np.zeros(m)
         want[k] = 1.0
         assert np.max(np.abs(e - want)) <= 1e-10
+
+
+@pytest.mark.parametrize("window", [16, 64])
+@pytest.mark.parametrize("m,n,seed", [(64, 256, 0), (257, 771, 2), (600, 1800, 5)])
+def test_devex_follows_oracle_path(spx, oracle, window, m, n, seed):
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, eps=1e-7, pricing=oracle.PRICING_DEVEX)
+    with spx.Context(A, b, c, eps=1e-7, window=window, pricing=spx.PRICING_DEVEX) as ctx:
+        r = ctx.solve()
+    assert int(r.status) == ref.status == 1
+    assert r.pivots == ref.pivots
+    assert list(r.b_ixs) == list(ref.b_ixs)
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+
+
+@pytest.mark.parametrize("rule", [1, 2])
+@pytest.mark.parametrize("m,n,seed", [(96, 300, 1), (300, 900, 4)])
+def test_devex_degenerate_lps(spx, oracle, rule, m, n, seed):
+    A, b, c = degenerate_lp(m, n, seed)
+    z_star = highs_opt(A, b, c)
+    with spx.Context(A, b, c, eps=1e-7, ratio_test=rule, pricing=spx.PRICING_DEVEX) as ctx:
+        r = ctx.solve(max_iter=20 * n)
+    assert r.status == spx.SolveStatus.OptimumFound
+    assert abs(r.z - z_star) <= 1e-9 * abs(z_star)
+    assert r.x_b.min() >= -1e-9
+
+
+def test_devex_stepwise_and_options(spx, oracle):
+    A, b, c = oracle.generate(64, 256, 0)
+    ref = oracle.solve(A, b, c, eps=1e-7, pricing=oracle.PRICING_DEVEX, trace_cap=10)
+    with spx.Context(A, b, c, eps=1e-7, pricing=spx.PRICING_DEVEX) as ctx:
+        for k in range(10):
+            p, e, opt = ctx.price()
+            assert not opt and p == ref.trace_p[k]
+            assert e < -1e-7  # the entering column's reduced cost, not the Devex key
+            q, st = ctx.pivot()
+            assert q == ref.trace_q[k]
+    with pytest.raises(spx.SimplexError):
+        spx.Context(A, b, c, window=-1, pricing=spx.PRICING_DEVEX)

@@ -177,3 +177,20 @@ def test_refactor_every_keeps_path(oracle):
     r = oracle.solve(A, b, c, refactor_every=20, trace_cap=1000)
     assert r.pivots == ref.pivots and np.array_equal(r.trace_q, ref.trace_q)
     assert abs(r.z - ref.z) <= 1e-11 * abs(ref.z)
+
+
+def test_devex_reaches_optimum(oracle, golden):
+    from lpgen import degenerate_lp, highs_opt
+
+    for case in golden["cases"][:9]:
+        A, b, c = oracle.generate(case["m"], case["n"], case["seed"])
+        r = oracle.solve(A, b, c, pricing=oracle.PRICING_DEVEX)
+        assert r.status == oracle.OPTIMUM_FOUND
+        assert abs(r.z - case["highs_z"]) <= 1e-9 * abs(case["highs_z"])
+        assert sorted(int(j) for j in r.b_ixs) == case["highs_basis"]
+    A, b, c = degenerate_lp(300, 900, 4)
+    z_star = highs_opt(A, b, c)
+    d = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED)
+    x = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED, pricing=oracle.PRICING_DEVEX)
+    assert abs(x.z - z_star) <= 1e-9 * abs(z_star)
+    assert x.pivots < d.pivots  # Devex needs fewer pivots on this degenerate LP (347 vs 1124)
