@@ -89,7 +89,9 @@ typedef struct spx_opts {
     double  feas_tol;     /* SPX_RATIO_HARRIS: primal feasibility tolerance
                              delta of the first pass (default 1e-9)          */
     int32_t pricing;      /* entering-column rule, SPX_PRICING_* (default DANTZIG) */
-    int32_t reserved[3];
+    int32_t loop_block;   /* tuning: threads per workgroup of the persistent loop
+                             kernel (512 / 1024), 0 = auto                     */
+    int32_t reserved[2];
 } spx_opts;
 
 /* Entering-column rules (README.md:16-17 "steepest edge").
@@ -129,6 +131,14 @@ typedef struct spx_opts {
                                (automatic when L*8 bytes do not fit in LDS)   */
 #define SPX_FLAG_SPLIT_TAIL 16 /* tuning: run the pivot tail as its own launch
                                   instead of the update kernel's last workgroup */
+#define SPX_FLAG_NO_PERSIST 32 /* tuning: never use the persistent loop kernel */
+#define SPX_FLAG_PERSIST 64    /* tuning: use the persistent cooperative loop kernel
+                                  (k_loop: one launch per window, two grid
+                                  barriers per pass instead of two kernels) where
+                                  it applies (window > 0, one rank, no Harris, no
+                                  stamps).  Default: only when y_w and the base
+                                  row do not both fit in LDS (m > ~9400, e.g. C5:
+                                  +7 %); at C3 the two-kernel pass is faster.   */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass
@@ -246,6 +256,14 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
 #define SPX_PHASES 13
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
+/* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]
+ * = 1): out[0] device milliseconds of the loop launches (hipEvents) and out[1]
+ * the passes they ran, since the last call; out[2..4] microseconds summed
+ * over passes of the in-kernel phases seen by workgroup 0 (s_memrealtime):
+ * pricing to grid barrier 1, FTRAN + ratio test to barrier 2, tail to the
+ * next pass; passes = passes with a phase split.  Resets. */
+int spx_loop_times(spx_ctx* ctx, double out[5], int64_t* passes);
+
 /* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this
  * rank (8*(m+1)*local non-basic columns), bytes_update: the B^-1 bytes per
  * pivot — 16*m*m for the explicit rank-1 update, or
@@ -257,8 +275,9 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * threads per workgroup, [2] pricing workgroups, [3] pricing LDS mode (0 y
  * in global, 1 y in LDS, 2 y and the window base row in LDS), [4] update
  * threads per workgroup, [5] update rows per wave, [6] update workgroups,
- * [7] passes per captured hipGraph (0 = eager). */
-#define SPX_CONFIG_FIELDS 8
+ * [7] passes per captured hipGraph (0 = eager), [8] persistent loop kernel
+ * in use (1) or not (0), [9] its threads per workgroup. */
+#define SPX_CONFIG_FIELDS 10
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:

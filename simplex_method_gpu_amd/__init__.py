@@ -32,6 +32,8 @@ FLAG_STAMPS = 2
 FLAG_GLOBAL_Y = 4
 FLAG_ROW_SHARD = 8
 FLAG_SPLIT_TAIL = 16
+FLAG_NO_PERSIST = 32
+FLAG_PERSIST = 64  # force the persistent loop kernel where it applies (default: auto)
 
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
@@ -126,7 +128,7 @@ class Context:
                  update_rows: int = 0, price_grid: int = 0, update_block: int = 0, stamps: bool = False,
                  global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
                  ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0,
-                 pricing: int = 0):
+                 pricing: int = 0, persist: bool | None = None, loop_block: int = 0):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -137,9 +139,11 @@ class Context:
         o.ratio_test, o.piv_tol, o.feas_tol = ratio_test, piv_tol, feas_tol  # RATIO_*
         o.refactor_every = refactor_every
         o.pricing = pricing  # PRICING_DANTZIG / PRICING_DEVEX
+        o.loop_block = loop_block
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
-                   | (FLAG_SPLIT_TAIL if split_tail else 0))
+                   | (FLAG_SPLIT_TAIL if split_tail else 0)
+                   | ({None: 0, True: FLAG_PERSIST, False: FLAG_NO_PERSIST}[persist]))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
@@ -257,6 +261,14 @@ class Context:
                 "tail_bookkeeping_us": out[7], "update_prologue_us": out[9], "update_drain_us": out[10],
                 "price_prologue_us": out[11], "price_drain_us": out[12]}
 
+    def loop_times(self):
+        """Persistent loop kernel (timing=True): launch ms + passes (hipEvents)
+        and the in-kernel phase split (microseconds summed over passes)."""
+        out, n = (ctypes.c_double * 5)(), ctypes.c_int64()
+        check(self._L.spx_loop_times(self._h, out, ctypes.byref(n)))
+        return {"loop_ms": out[0], "loop_passes": int(out[1]), "price_us": out[2], "ftran_us": out[3],
+                "tail_us": out[4], "clock_passes": n.value}
+
     def pass_times(self):
         """Event-timed sums (timing=True): pricing kernel, pricing + MINLOC
         exchange, update kernel (ms), and the number of timed passes."""
@@ -275,10 +287,10 @@ class Context:
 
     def config(self):
         """Resolved representation and launch geometry (spx_config)."""
-        out = (ctypes.c_int32 * 8)()
+        out = (ctypes.c_int32 * 10)()
         check(self._L.spx_config(self._h, out))
         keys = ("window", "price_block", "price_grid", "price_lds", "update_block", "update_rows", "update_grid",
-                "graph_batch")
+                "graph_batch", "persistent", "loop_block")
         return dict(zip(keys, list(out)))
 
 

@@ -36,7 +36,8 @@ class SpxOpts(ctypes.Structure):
         ("piv_tol", ctypes.c_double),
         ("feas_tol", ctypes.c_double),
         ("pricing", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 3),
+        ("loop_block", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 
@@ -64,6 +65,7 @@ SIGNATURES = {
     "spx_info": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p]),
     "spx_config": (ctypes.c_int, [_p, _p]),
     "spx_phase_times": (ctypes.c_int, [_p, _p]),
+    "spx_loop_times": (ctypes.c_int, [_p, _p, _p]),
     "spx_shard_range": (ctypes.c_int, [_i64, _i64, _i32, _i32, _p]),
     "spx_minloc_merge": (ctypes.c_int, [_p, _p, _i32, _p, _p]),
     "spx_last_error": (ctypes.c_char_p, []),

@@ -22,6 +22,7 @@
 #include "spx_device.h"
 #include "spx_kernels.h"
 #include "spx_reinv.h"
+#include "spx_loop.h"
 
 using namespace spx;
 
@@ -123,6 +124,16 @@ struct spx_ctx {
     int32_t status = SPX_STATUS_MAX_ITER;
     bool stepped_price = false;
     int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
+
+    // persistent loop kernel (spx_loop.h): window mode, one rank
+    LoopCfg lcfg{};
+    LoopArgs la{};
+    bool persist = false;
+    double loop_clock[3] = {0.0, 0.0, 0.0};  // timing: phase A / B / C microseconds (in-kernel clock)
+    int64_t loop_clock_passes = 0;
+    std::vector<hipEvent_t> ev_loop;
+    std::vector<int32_t> ev_loop_passes;
+    size_t n_loop = 0;
 
     // basis reinversion (spx_reinv.h): work buffers allocated on first use
     RvParams rv{};
@@ -368,6 +379,23 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
 
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
+    // the persistent loop kernel replaces the two-kernel pass where it applies
+    if (P.win && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
+        !(x->opts.flags & SPX_FLAG_NO_PERSIST)) {
+        x->lcfg.block = x->opts.loop_block;
+        HIP_TRY(loop_prepare(P, x->cus, x->lcfg));
+        // measured (tools/loop_sweep.sh): the persistent loop wins once the
+        // base row is read from L2 (C5: 729 vs 681 it/s) and loses at C3
+        // (8.3k vs 9.3k it/s), so by default only then
+        const bool want = (x->opts.flags & SPX_FLAG_PERSIST) || !x->lcfg.lds_r;
+        if (x->lcfg.ok && want) {
+            SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
+            SPX_TRY(x->alloc(&x->la.up, (size_t)x->lcfg.grid));
+            SPX_TRY(x->alloc(&x->la.ls, 1));
+            SPX_TRY(x->alloc(&x->la.clock, (size_t)(3 * 64)));
+            x->persist = true;
+        }
+    }
     if (x->opts.flags & SPX_FLAG_STAMPS) {
         SPX_TRY(x->alloc(&P.stamps, 32));
         SPX_TRY(reset_stamps(x));
@@ -552,8 +580,68 @@ int iterate(spx_ctx* x, int64_t k) {
     return SPX_OK;
 }
 
+// Persistent loop: one cooperative launch per window (k_loop), folds between.
+int iterate_persist(spx_ctx* x, int64_t k) {
+    int64_t left = k;
+    while (left > 0) {
+        const bool fold = fold_due(x);
+        if (fold) {
+            HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+            x->nw = 1;
+        }
+        const int64_t np = std::min<int64_t>(left, x->P.win - x->nw);
+        LoopArgs a = x->la;
+        a.npasses = (int32_t)np;
+        if (!x->timing) a.clock = nullptr;
+        HIP_TRY(hipMemsetAsync(a.ls, 0, sizeof(LoopState), x->stream));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (x->timing) {
+            if (x->ev_loop.size() < 2 * (x->n_loop + 1)) {
+                for (int i = 0; i < 2; ++i) {
+                    hipEvent_t e;
+                    HIP_TRY(hipEventCreate(&e));
+                    x->ev_loop.push_back(e);
+                }
+                x->ev_loop_passes.push_back(0);
+            }
+            e0 = x->ev_loop[2 * x->n_loop];
+            e1 = x->ev_loop[2 * x->n_loop + 1];
+            x->ev_loop_passes[x->n_loop] = (int32_t)np;
+            ++x->n_loop;
+            HIP_TRY(hipEventRecord(e0, x->stream));
+        }
+        HIP_TRY(launch_loop(x->P, a, x->lcfg, x->stream));
+        if (e1) HIP_TRY(hipEventRecord(e1, x->stream));
+        if (x->timing) {  // phase split from workgroup 0's clock (s_memrealtime, 100 MHz)
+            unsigned long long ck[3 * 64];
+            LoopState ls{};
+            HIP_TRY(hipStreamSynchronize(x->stream));
+            HIP_TRY(hipMemcpy(&ls, a.ls, sizeof(ls), hipMemcpyDeviceToHost));
+            const int done = std::min<int>(ls.passes, 64);
+            HIP_TRY(hipMemcpy(ck, a.clock, sizeof(unsigned long long) * 3 * (size_t)done, hipMemcpyDeviceToHost));
+            for (int i = 0; i < done; ++i) {
+                x->loop_clock[0] += 1e-2 * (double)(ck[3 * i + 1] - ck[3 * i]);
+                x->loop_clock[1] += 1e-2 * (double)(ck[3 * i + 2] - ck[3 * i + 1]);
+                if (i + 1 < done) x->loop_clock[2] += 1e-2 * (double)(ck[3 * i + 3] - ck[3 * i + 2]);
+            }
+            x->loop_clock_passes += done;
+        }
+        x->nw += (int)np;
+        left -= np;
+    }
+    SPX_TRY(read_state(x));
+    LoopState ls{};
+    HIP_TRY(hipMemcpy(&ls, x->la.ls, sizeof(ls), hipMemcpyDeviceToHost));
+    if (ls.err) return fail(SPX_ERR_STATE, "persistent loop: a grid barrier timed out");
+    return SPX_OK;
+}
+
 int iterate_raw(spx_ctx* x, int64_t k) {
     if (x->status != SPX_STATUS_MAX_ITER || k <= 0) return SPX_OK;
+    if (x->persist && !x->stepped_price) {
+        SPX_TRY(set_limit(x, x->pivots + k));
+        return iterate_persist(x, k);
+    }
     if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
     SPX_TRY(set_limit(x, x->pivots + k));
     // exactly k passes: whole captured batches, then the remainder eagerly.
@@ -679,7 +767,7 @@ int reinvert_current(spx_ctx* x) {
 
 int create_tail(spx_ctx* x) {
     SPX_TRY(do_reset(x));
-    if (x->opts.nranks == 1) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
+    if (x->opts.nranks == 1 && !x->persist) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
     return SPX_OK;
 }
 
@@ -1090,6 +1178,29 @@ int spx_pass_times(spx_ctx* x, double out[3], int64_t* passes) {
     return SPX_OK;
 }
 
+int spx_loop_times(spx_ctx* x, double out[5], int64_t* passes) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    double ms = 0.0;
+    int64_t np = 0;
+    for (size_t i = 0; i < x->n_loop; ++i) {
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, x->ev_loop[2 * i], x->ev_loop[2 * i + 1]));
+        ms += t;
+        np += x->ev_loop_passes[i];
+    }
+    x->n_loop = 0;
+    out[0] = ms;
+    out[1] = (double)np;
+    out[2] = x->loop_clock[0];
+    out[3] = x->loop_clock[1];
+    out[4] = x->loop_clock[2];
+    if (passes) *passes = x->loop_clock_passes;
+    x->loop_clock[0] = x->loop_clock[1] = x->loop_clock[2] = 0.0;
+    x->loop_clock_passes = 0;
+    return SPX_OK;
+}
+
 int spx_kernel_times(spx_ctx* x, double* price_ms, int64_t* np, double* update_ms, int64_t* nu) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
     HIP_TRY(hipStreamSynchronize(x->stream));
@@ -1155,6 +1266,8 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[5] = x->ucfg.rows;
     out[6] = x->ucfg.grid;
     out[7] = x->batch;
+    out[8] = x->persist ? 1 : 0;
+    out[9] = x->persist ? x->lcfg.block : 0;
     return SPX_OK;
 }
 

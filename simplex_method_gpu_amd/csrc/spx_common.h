@@ -1,0 +1,121 @@
+// spx_common.h — device helpers shared by the loop kernels (spx_kernels.hip)
+// and the persistent loop kernel (spx_loop.hip): vector types, cache-policy
+// loads/stores, wave reductions, agent-scope hand-off primitives and the
+// pieces of the deferred pivot (one definition, so every consumer produces
+// the same bits).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "spx_device.h"
+
+namespace spx {
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+// Cache policy of the three big streams (compile-time; tools/policy_sweep.sh
+// builds the variants): 1 = non-temporal, 0 = default.  Measured at C3:
+// non-temporal loads of A cut k_price 93 -> 68 us, of B^-1 k_update 69 -> 56 us.
+#ifndef SPX_NT_A
+#define SPX_NT_A 1      // pricing reads of A
+#endif
+#ifndef SPX_NT_BLOAD
+#define SPX_NT_BLOAD 1  // update reads of B_old
+#endif
+#ifndef SPX_NT_BSTORE
+#define SPX_NT_BSTORE 1 // update writes of B_new
+#endif
+
+template <int NT>
+__device__ __forceinline__ dbl2 ld2(const dbl2* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+// two butterflies interleaved (their cross-lane latencies overlap)
+__device__ __forceinline__ void wave_sum2(double& a, double& b) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ta = __shfl_xor(a, off, 64);
+        const double tb = __shfl_xor(b, off, 64);
+        a += ta;
+        b += tb;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ bool stopped(const DevState* st) {
+    return st->status != ST_RUNNING || st->iter >= st->limit;
+}
+
+__device__ __forceinline__ unsigned long long rtime() { return __builtin_amdgcn_s_memrealtime(); }
+
+// compute_E_q (v4:210-215)
+__device__ __forceinline__ double eta_entry(double a_i, int64_t i, int64_t q, double aq) {
+    return (i != q) ? (-a_i / aq) : (1.0 / aq - 1.0);
+}
+// y += s_y r (v4:356)
+__device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
+    dbl2 o;
+    o.x = fma(s_y, r.x, y.x);
+    o.y = fma(s_y, r.y, y.y);
+    return o;
+}
+
+// Merge of ratio-test partials: argmin on (theta, idx) carrying the winner's
+// scalars; nonpos and T summed.  Callers fix the order of the sums.
+__device__ __forceinline__ void upd_merge(UpdPartial& a, const UpdPartial& b) {
+    if (argmin_better(b.theta, b.idx, a.theta, a.idx)) {
+        a.theta = b.theta;
+        a.idx = b.idx;
+        a.a_w = b.a_w;
+        a.cb_w = b.cb_w;
+        a.bix_w = b.bix_w;
+    }
+    a.nonpos += b.nonpos;
+    a.T += b.T;
+}
+__device__ __forceinline__ UpdPartial upd_empty() { return UpdPartial{INFINITY, INT64_MAX, 0, 0.0, 0.0, 0.0, -1, 0}; }
+__device__ __forceinline__ UpdPartial upd_shfl_xor(const UpdPartial& v, int off) {
+    UpdPartial o;
+    o.theta = __shfl_xor(v.theta, off, 64);
+    o.idx = __shfl_xor(v.idx, off, 64);
+    o.nonpos = __shfl_xor(v.nonpos, off, 64);
+    o.T = __shfl_xor(v.T, off, 64);
+    o.a_w = __shfl_xor(v.a_w, off, 64);
+    o.cb_w = __shfl_xor(v.cb_w, off, 64);
+    o.bix_w = __shfl_xor(v.bix_w, off, 64);
+    o.pad = 0;
+    return o;
+}
+
+// y-update scalar (v4:352-355): c_B_new.E_q + c_p - c_Bq with E_i = -alpha_i /
+// alpha_q (i != q), E_q = 1/alpha_q - 1, c_B_new[q] = c_p, evaluated from the
+// gathered T = sum_i c_B[i] alpha_i (so the tail needs no O(m) pass):
+// c_B_new.E_q = -(T - c_Bq alpha_q)/alpha_q + c_p (1/alpha_q - 1).
+__device__ __forceinline__ double y_scalar(double T, double aq, double c_bq, double c_p) {
+    const double sy = -(T - c_bq * aq) / aq + c_p * (1.0 / aq - 1.0);
+    return sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
+}
+
+}  // namespace spx

@@ -28,25 +28,11 @@
 #include <math.h>
 
 #include "spx_device.h"
+#include "spx_common.h"
 #include "spx_fold.h"
 #include "spx_kernels.h"
 
 namespace spx {
-
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-// Cache policy of the three big streams (compile-time; tools/policy_sweep.sh
-// builds the variants): 1 = non-temporal, 0 = default.  Measured at C3:
-// non-temporal loads of A cut k_price 93 -> 68 us, of B^-1 k_update 69 -> 56 us.
-#ifndef SPX_NT_A
-#define SPX_NT_A 1      // pricing reads of A
-#endif
-#ifndef SPX_NT_BLOAD
-#define SPX_NT_BLOAD 1  // update reads of B_old
-#endif
-#ifndef SPX_NT_BSTORE
-#define SPX_NT_BSTORE 1 // update writes of B_new
-#endif
 
 // B^-1 storage: 1 = one buffer updated in place (the pivot row the stream
 // needs is staged into P.rbuf by k_price); 0 = ping-pong between B0 and B1.
@@ -56,55 +42,16 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef SPX_LDS_BATCH
 #define SPX_LDS_BATCH 4  // eta-window pricing: y / base-row LDS reads issued together
 #endif
+#ifndef SPX_WIN_APLDS
+#define SPX_WIN_APLDS 0  // eta-window FTRAN: A_p from LDS (1) or through L1/L2 (0)
+#endif
 #ifndef SPX_WIN_U1
 #define SPX_WIN_U1 16  // eta-window FTRAN stream, 1 row per wave: dbl2 loads per lane per round trip
 #endif
 bool kernels_inplace() { return SPX_INPLACE != 0; }
 
-template <int NT>
-__device__ __forceinline__ dbl2 ld2(const dbl2* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <int NT>
-__device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-// two butterflies interleaved (their cross-lane latencies overlap)
-__device__ __forceinline__ void wave_sum2(double& a, double& b) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ta = __shfl_xor(a, off, 64);
-        const double tb = __shfl_xor(b, off, 64);
-        a += ta;
-        b += tb;
-    }
-}
-
-template <typename T>
-__device__ __forceinline__ void st_agent(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T* p) {
-    return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-__device__ __forceinline__ bool stopped(const DevState* st) {
-    return st->status != ST_RUNNING || st->iter >= st->limit;
-}
-
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
 // launch, slot[1] += (last-workgroup ticket - start), slot[2] += tail duration.
-__device__ __forceinline__ unsigned long long rtime() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ void stamp_start(unsigned long long* slot) {
     if (slot && threadIdx.x == 0) atomicMin(&slot[0], rtime());
 }
@@ -147,18 +94,6 @@ __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, 
 // Pieces of the deferred pivot (one definition, so every consumer — k_price,
 // k_update, k_flush, k_materialize — produces the same bits)
 // ---------------------------------------------------------------------------
-// compute_E_q (v4:210-215)
-__device__ __forceinline__ double eta_entry(double a_i, int64_t i, int64_t q, double aq) {
-    return (i != q) ? (-a_i / aq) : (1.0 / aq - 1.0);
-}
-// y += s_y r (v4:356)
-__device__ __forceinline__ dbl2 y_apply(double s_y, dbl2 r, dbl2 y) {
-    dbl2 o;
-    o.x = fma(s_y, r.x, y.x);
-    o.y = fma(s_y, r.y, y.y);
-    return o;
-}
-
 // ---------------------------------------------------------------------------
 // Pricing + entering argmin
 // ---------------------------------------------------------------------------
@@ -489,33 +424,6 @@ __device__ double block_sum(double a, double* sa) {
     return t;
 }
 
-// Merge of ratio-test partials: argmin on (theta, idx) carrying the winner's
-// scalars; nonpos and T summed.  Callers fix the order of the sums.
-__device__ __forceinline__ void upd_merge(UpdPartial& a, const UpdPartial& b) {
-    if (argmin_better(b.theta, b.idx, a.theta, a.idx)) {
-        a.theta = b.theta;
-        a.idx = b.idx;
-        a.a_w = b.a_w;
-        a.cb_w = b.cb_w;
-        a.bix_w = b.bix_w;
-    }
-    a.nonpos += b.nonpos;
-    a.T += b.T;
-}
-__device__ __forceinline__ UpdPartial upd_empty() { return UpdPartial{INFINITY, INT64_MAX, 0, 0.0, 0.0, 0.0, -1, 0}; }
-__device__ __forceinline__ UpdPartial upd_shfl_xor(const UpdPartial& v, int off) {
-    UpdPartial o;
-    o.theta = __shfl_xor(v.theta, off, 64);
-    o.idx = __shfl_xor(v.idx, off, 64);
-    o.nonpos = __shfl_xor(v.nonpos, off, 64);
-    o.T = __shfl_xor(v.T, off, 64);
-    o.a_w = __shfl_xor(v.a_w, off, 64);
-    o.cb_w = __shfl_xor(v.cb_w, off, 64);
-    o.bix_w = __shfl_xor(v.bix_w, off, 64);
-    o.pad = 0;
-    return o;
-}
-
 // Leaving argmin over the k_update workgroup partials + unbounded count
 // (v4:317-325), carrying the winner's scalars.  One dependent round trip
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
@@ -563,15 +471,6 @@ struct UpdLds {
     static constexpr size_t last = red + sizeof(UpdPartial) * WAVES;    // int
     static constexpr size_t bytes = last + 16;
 };
-
-// y-update scalar (v4:352-355): c_B_new.E_q + c_p - c_Bq with E_i = -alpha_i /
-// alpha_q (i != q), E_q = 1/alpha_q - 1, c_B_new[q] = c_p, evaluated from the
-// gathered T = sum_i c_B[i] alpha_i (so the tail needs no O(m) pass):
-// c_B_new.E_q = -(T - c_Bq alpha_q)/alpha_q + c_p (1/alpha_q - 1).
-__device__ __forceinline__ double y_scalar(double T, double aq, double c_bq, double c_p) {
-    const double sy = -(T - c_bq * aq) / aq + c_p * (1.0 / aq - 1.0);
-    return sy + (c_p - c_bq);  // compute_scalar (v4:195-197)
-}
 
 // Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and
 // the deferred pivot state (spx_device.h).  One thread.
@@ -645,6 +544,40 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
 template <int BLOCK>
 __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int par, const double* a_prev,
                                unsigned char* smem, int nparts);
+
+// Eta-window FTRAN rows: acc[u] += B_w[row u,:] . A_p for R full rows, U dbl2
+// loads of B per lane per round trip.  a: A_p in global memory or in LDS.
+template <int U, int R>
+__device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2* __restrict__ src, int64_t base,
+                                         int64_t L2, int lane, double (&acc)[R]) {
+    int64_t k = lane;
+    for (; k + (U - 1) * 64 < L2; k += U * 64) {
+        dbl2 av[U], bv[U][R];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            av[t] = a[k + t * 64];
+#pragma unroll
+            for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                acc[u] = fma(bv[t][u].x, av[t].x, acc[u]);
+                acc[u] = fma(bv[t][u].y, av[t].y, acc[u]);
+            }
+        }
+    }
+    for (; k < L2; k += 64) {
+        const dbl2 av = a[k];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const dbl2 bv = src[base + u * L2 + k];
+            acc[u] = fma(bv.x, av.x, acc[u]);
+            acc[u] = fma(bv.y, av.y, acc[u]);
+        }
+    }
+}
 
 template <int BLOCK, int R, bool RS, bool WIN>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
@@ -746,36 +679,21 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 P.Wt[P.b_ixs[i] * KW + tau] = (i == q) ? aq : 0.0;
             }
         }
+        // A_p staged in LDS once per workgroup (SPX_WIN_APLDS) instead of
+        // every wave re-reading it through L1/L2 beside the B stream
+        const bool aplds = SPX_WIN_APLDS && L * 8 <= 65536;
+        if (SPX_WIN_APLDS && aplds) {
+            dbl2* d = reinterpret_cast<dbl2*>(smem + Lds::bytes);
+            for (int64_t kk = tid; kk < L2; kk += BLOCK) d[kk] = ap[kk];
+            __syncthreads();
+        }
         if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
-            int64_t k = lane;
-            for (; k + (U - 1) * 64 < L2; k += U * 64) {
-                dbl2 av[U], bv[U][R];
-#pragma unroll
-                for (int t = 0; t < U; ++t) {
-                    av[t] = ap[k + t * 64];
-#pragma unroll
-                    for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
-                }
-#pragma unroll
-                for (int t = 0; t < U; ++t) {
-#pragma unroll
-                    for (int u = 0; u < R; ++u) {
-                        acc[u] = fma(bv[t][u].x, av[t].x, acc[u]);
-                        acc[u] = fma(bv[t][u].y, av[t].y, acc[u]);
-                    }
-                }
-            }
-            for (; k < L2; k += 64) {
-                const dbl2 av = ap[k];
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    const dbl2 bv = src[base + u * L2 + k];
-                    acc[u] = fma(bv.x, av.x, acc[u]);
-                    acc[u] = fma(bv.y, av.y, acc[u]);
-                }
-            }
+            if (SPX_WIN_APLDS && aplds)
+                win_rows<U, R>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc);
+            else
+                win_rows<U, R>(ap, src, base, L2, lane, acc);
         } else if (nvalid > 0) {
             for (int64_t k = lane; k < L2; k += 64) {
                 const dbl2 av = ap[k];
@@ -1388,7 +1306,7 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
 
 template <int BLOCK, int R, bool RS, bool WIN>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const size_t lds = UpdLds<BLOCK>::bytes;
+    const size_t lds = UpdLds<BLOCK>::bytes + ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0);
     if (e0 || e1) {
         hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
                               P);

@@ -20,12 +20,13 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
+@pytest.mark.parametrize("persist", [False, True])
 @pytest.mark.parametrize("window", WINDOWS)
 @pytest.mark.parametrize("m,n,seed,k", [(257, 771, 2, 150), (1000, 3000, 3, 140)])
-def test_window_state_matches_oracle(spx, oracle, window, m, n, seed, k):
+def test_window_state_matches_oracle(spx, oracle, window, m, n, seed, k, persist):
     A, b, c = oracle.generate(m, n, seed)
     ref = oracle.solve(A, b, c, max_iter=k, eps=1e-7, want_state=True, trace_cap=k)
-    with spx.Context(A, b, c, eps=1e-7, window=window) as ctx:
+    with spx.Context(A, b, c, eps=1e-7, window=window, persist=persist) as ctx:
         st, piv = ctx.iterate(k)
         s = ctx.state(binv=True)
         e = ctx.reduced_costs()
@@ -76,16 +77,28 @@ def test_window_readback_mid_window_then_continue(spx, oracle):
 
 @pytest.mark.parametrize("window", [16, 32])
 def test_window_graph_eager_bit_identical(spx, window):
+    """Two-kernel passes (persist=False): graph replay, eager launches and every
+    pricing geometry give the same bits.  The persistent loop kernel (k_loop,
+    both workgroup sizes) groups the ratio test's c_B.alpha sum by its own
+    geometry: same pivots, values within 1e-12."""
     m, n, seed, k = 300, 1200, 7, 130
     runs = []
     for kw in (dict(), dict(graph_batch=-1), dict(graph_batch=5), dict(price_grid=3), dict(price_block=1024)):
-        with spx.Context(m=m, n=n, seed=seed, window=window, **kw) as ctx:
+        with spx.Context(m=m, n=n, seed=seed, window=window, persist=False, **kw) as ctx:
+            assert ctx.config()["persistent"] == 0
             ctx.iterate(k)
             runs.append((kw, ctx.state(binv=True)))
     s0 = runs[0][1]
     for kw, s in runs[1:]:
         for key in ("b_ixs", "x_b", "y", "binv"):
             assert np.array_equal(s[key], s0[key]), (kw, key)
+    with spx.Context(m=m, n=n, seed=seed, window=window, persist=True) as ctx:
+        assert ctx.config()["persistent"] == 1
+        st, piv = ctx.iterate(k)
+        s = ctx.state(binv=True)
+    assert piv == k and np.array_equal(s["b_ixs"], s0["b_ixs"])
+    for key in ("x_b", "y", "binv"):
+        assert _rel(s[key], s0[key]) <= 1e-12, key
 
 
 def test_window_matches_explicit_update(spx):
@@ -134,7 +147,7 @@ def test_window_shard_group_matches_single_rank(spx, G, m, n, k):
     """Column-sharded pricing: the winner's window coefficients travel in the
     MINLOC record; every shard reproduces the single-rank window run bitwise."""
     seed = 11
-    with spx.Context(m=m, n=n, seed=seed, window=16) as ref:
+    with spx.Context(m=m, n=n, seed=seed, window=16, persist=False) as ref:
         rst, rpiv = ref.iterate(k)
         rs = ref.state(binv=True)
     ctxs = [spx.Context(m=m, n=n, seed=seed, rank=g, nranks=G, window=16) for g in range(G)]
