@@ -118,6 +118,8 @@ def main():
         ctx.iterate(args.warmup)
         if events:
             ctx.pass_times()  # drop the warmup's events
+            if ctx.config()["persistent"]:
+                ctx.loop_times()
         info0 = ctx.info()
         _, piv0 = ctx.iterate(0)
         barrier()
@@ -127,7 +129,18 @@ def main():
         torch.cuda.synchronize()
         barrier()
         dt = reduce_max([time.perf_counter() - t0])[0]
-        pt = ctx.pass_times() if events else None
+        pt = None
+        if events:
+            pt = ctx.pass_times()
+            if ctx.config()["persistent"]:
+                # persistent loop kernel (k_loop): phases timed in-kernel by
+                # workgroup 0 (pricing to grid barrier 1, FTRAN to barrier 2),
+                # launches by hipEvents
+                lt = ctx.loop_times()
+                np_ = max(lt["clock_passes"], 1)
+                pt = {"passes": np_, "price_ms": 1e-3 * lt["price_us"],
+                      "price_minloc_ms": 1e-3 * lt["price_us"], "update_ms": 1e-3 * lt["ftran_us"],
+                      "loop_ms_per_pass": lt["loop_ms"] / max(lt["loop_passes"], 1)}
         info1 = ctx.info()
         return dt, piv1 - piv0, pt, 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"])
 
@@ -180,6 +193,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(m, n, args.seed, args.cpu_seconds)
+        cpu["glpk"] = glpk_status()
 
     if rank == 0:
         out = {
@@ -211,7 +225,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_price (pricing GEMV + entering argmin), rank 0",
+                "kernel": ("k_loop pricing phase (in-kernel clock, workgroup 0), rank 0" if cfg.get("persistent")
+                           else "k_price (pricing GEMV + entering argmin), rank 0"),
                 "achieved": price_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -241,6 +256,25 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def glpk_status():
+    """The reference's CPU baseline is GLPK (solver_glpk.cpp).  Its counterpart
+    ./solver_glpk binds libglpk at run time and exits 3 when it is absent; the
+    oracle then stands in (kind "port") and this says why."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "solver_glpk")
+    if not os.path.exists(exe):
+        return "solver_glpk not built"
+    try:
+        r = subprocess.run([exe, "--text", os.path.join(ROOT, "tests", "golden", "sample.txt")],
+                           capture_output=True, text=True, timeout=60)
+    except (OSError, subprocess.SubprocessError) as e:
+        return f"solver_glpk failed: {e}"
+    if r.returncode == 3:
+        return "unavailable: libglpk not loadable on this host (solver_glpk exit 3)"
+    return "available" if r.returncode == 0 else f"solver_glpk exit {r.returncode}"
 
 
 def cpu_baseline(m, n, seed, budget_s):

@@ -474,15 +474,39 @@ struct UpdLds {
 
 // Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and
 // the deferred pivot state (spx_device.h).  One thread.
+// Scalars of the bookkeeping that only depend on the entering column, loaded
+// by every k_update workgroup at its start so the last one's tail does not
+// wait on a chain of dependent global loads.
+struct TailPre {
+    bool valid;
+    double c_p;
+    int32_t cnt, kp, last;
+    double wp;  // Devex: the entering column's weight
+};
+
+__device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState* st, int64_t p) {
+    TailPre t{false, 0.0, 0, -1, -1, 0.0};
+    if (p < 0 || p >= P.n) return t;
+    t.c_p = P.c[p];
+    t.cnt = st->nb_count;
+    if (owns_col(P, p)) {
+        t.kp = P.nb_pos[p];
+        t.last = P.nb_list[t.cnt - 1];
+    }
+    if (P.devex) t.wp = P.W[p];
+    t.valid = true;
+    return t;
+}
+
 __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st, int64_t p, int64_t q,
                                                   int64_t leave, double aq, double s_y, double min_e,
-                                                  int64_t it) {
-    P.c_B[q] = P.c[p];
+                                                  int64_t it, const TailPre* pre = nullptr) {
+    P.c_B[q] = pre ? pre->c_p : P.c[p];
     P.b_ixs[q] = p;
-    int cnt = st->nb_count;
+    int cnt = pre ? pre->cnt : st->nb_count;
     if (owns_col(P, p)) {
-        const int kp = P.nb_pos[p];
-        const int last = P.nb_list[cnt - 1];
+        const int kp = pre ? pre->kp : P.nb_pos[p];
+        const int last = pre ? pre->last : P.nb_list[cnt - 1];
         P.nb_list[kp] = last;
         P.nb_pos[last] = kp;
         P.nb_pos[p] = -1;
@@ -506,7 +530,7 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
     st->xb_applied = it;
     if (P.devex) {
         st->leave = leave;
-        st->wp = P.W[p];
+        st->wp = pre ? pre->wp : P.W[p];
     }
     st->p = p;
     st->q = q;
@@ -519,7 +543,7 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
 // vector updates are deferred (spx_device.h).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            unsigned char* smem, int nparts) {
+                            unsigned char* smem, int nparts, const TailPre* pre = nullptr) {
     unsigned long long tm = P.stamps ? rtime() : 0;
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
     const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
@@ -536,7 +560,8 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
         st_agent(&st->ticket_update, 0u);
         return;
     }
-    pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, P.c[p]), min_e, it);
+    const double c_p = pre ? pre->c_p : P.c[p];
+    pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, c_p), min_e, it, pre);
     st_agent(&st->ticket_update, 0u);
     tail_mark(P, 1, tm);
 }
@@ -642,12 +667,23 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t lr0 = ((int64_t)blockIdx.x * WAVES + wave) * R;
     const int64_t gr0 = (RS ? P.r0 : 0) + lr0;
     const int nvalid = (int)((lr0 >= nrows) ? 0 : ((nrows - lr0 < R) ? (nrows - lr0) : R));
-    double ei[R], acc[R];
+    double ei[R], acc[R], cbv[R], xbv[R];
+    int64_t bixv[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
         ei[u] = (pend && u < nvalid) ? eta_entry(a_prev[gr0 + u], gr0 + u, qp, aqp) : 0.0;
         acc[u] = 0.0;
+        // row scalars of the epilogue, loaded ahead of the stream
+        cbv[u] = u < nvalid ? P.c_B[gr0 + u] : 0.0;
+        xbv[u] = u < nvalid ? P.x_b[gr0 + u] : 0.0;
+        bixv[u] = u < nvalid ? P.b_ixs[gr0 + u] : -1;
     }
+    double ucv[R];  // eta window: this row's U coefficients of the earlier window pivots
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+        ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
+    TailPre tpre{false, 0.0, 0, -1, -1, 0.0};
+    if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st, p);
     const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
@@ -708,7 +744,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         for (int u = 0; u < R; ++u) {
             if (u < nvalid) {
                 const int64_t li = lr0 + u;
-                const double cu = lane < tau ? P.U[li * KW + lane] : (lane == tau ? ei[u] : 0.0);
+                const double cu = lane < tau ? ucv[u] : (lane == tau ? ei[u] : 0.0);
                 acc[u] = fma(cu, wl, acc[u]);
                 if (pend && lane == 0) P.U[li * KW + tau] = ei[u];
             }
@@ -785,8 +821,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         if (u < nvalid) {
             const double a = wave_sum(acc[u]);
             const int64_t i = gr0 + u;
-            const double cb = P.c_B[i];
-            double xb = P.x_b[i];
+            const double cb = cbv[u];
+            double xb = xbv[u];
             if (upd_x) xb = fma(s_x, ei[u], xb);
             if (lane == 0) {
                 a_new[i] = a;  // read back by the next pass (own row) / k_flush
@@ -801,7 +837,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 wp.idx = i;
                 wp.a_w = a;
                 wp.cb_w = cb;
-                wp.bix_w = P.b_ixs[i];
+                wp.bix_w = bixv[u];
             }
         }
     }
@@ -843,7 +879,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if constexpr (RS)
         update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem, gridDim.x);
     else
-        update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x);
+        update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
     stamp_tail(slot, t_tail, win);
 }
 
