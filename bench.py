@@ -158,7 +158,9 @@ def main():
 
     if piv_g > 0 and dt_g / piv_g <= dt_e / max(piv_e, 1):
         best_dt, best_piv = dt_g, piv_g
-        mode = "hipGraph replay" if world == 1 else "eager + RCCL all-gather"
+        mode = ("hipGraph replay" if world == 1 else
+                ("hipGraph replay incl. RCCL all-gathers" if cfg.get("graph_batch", 0) > 0 else
+                 "eager + RCCL all-gather"))
     else:
         best_dt, best_piv, mode = dt_e, piv_e, "eager + hipExtLaunchKernel events"
     value = best_piv / best_dt if best_dt > 0 else 0.0

@@ -67,8 +67,9 @@ typedef struct spx_opts {
     int32_t device;       /* HIP device ordinal; -1 = keep the current device  */
     int32_t rank;         /* pricing shard of this process (default 0)         */
     int32_t nranks;       /* number of shards (default 1)                      */
-    int32_t graph_batch;  /* iterations per captured hipGraph; 0 = auto,
-                             -1 = eager launches                               */
+    int32_t graph_batch;  /* iterations per captured hipGraph; 0 = auto (16,
+                             RCCL calls captured too; a capture RCCL refuses
+                             falls back to eager), -1 = eager launches       */
     int32_t price_block;  /* tuning: threads per pricing workgroup, 0 = auto   */
     int32_t update_rows;  /* tuning: B^-1 rows per wave in the update, 0 = auto */
     int32_t price_grid;   /* tuning: pricing workgroups, 0 = auto              */
@@ -139,6 +140,10 @@ typedef struct spx_opts {
                                   stamps).  Default: only when y_w and the base
                                   row do not both fit in LDS (m > ~9400, e.g. C5:
                                   +7 %); at C3 the two-kernel pass is faster.   */
+#define SPX_FLAG_COMM1 128 /* test: with nranks == 1, run the MINLOC exchange through
+                              RCCL anyway (spx_attach_comm with a one-rank id), so
+                              the communicator path, graph-captured RCCL calls
+                              included, can be checked on one GPU            */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass

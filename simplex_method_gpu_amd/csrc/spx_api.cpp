@@ -102,6 +102,8 @@ struct spx_ctx {
     // multi-rank
     ncclComm_t comm = nullptr;
     bool comm_ready = false;
+    bool use_comm = false;  // MINLOC through RCCL: nranks > 1, or SPX_FLAG_COMM1 (one-rank test of that path)
+    bool graph_fallback = false;  // a capture with RCCL calls failed: eager passes
 
     // graph replay of `batch` passes
     hipGraphExec_t graph_exec = nullptr;
@@ -381,7 +383,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
     // the persistent loop kernel replaces the two-kernel pass where it applies
     if (P.win && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
-        !(x->opts.flags & SPX_FLAG_NO_PERSIST)) {
+        !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
         x->lcfg.block = x->opts.loop_block;
         HIP_TRY(loop_prepare(P, x->cus, x->lcfg));
         // measured (tools/loop_sweep.sh): the persistent loop wins once the
@@ -411,12 +413,15 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         P.rs_recv = rb;
         x->rs_recv = rb;
     }
+    x->use_comm = G > 1 || (x->opts.flags & SPX_FLAG_COMM1);
     P.price_out = x->send;
-    P.price_in = (G == 1) ? x->send : x->recv;
+    P.price_in = x->use_comm ? x->recv : x->send;
     P.nin = G;
 
+    // passes (RCCL calls included) are captured into hipGraphs of 16; a
+    // capture that fails falls back to eager launches (build_graph)
     int gb = x->opts.graph_batch;
-    if (gb == 0) gb = (G > 1) ? -1 : 16;  // RCCL passes are launched eagerly unless asked
+    if (gb == 0) gb = 16;
     x->batch = (gb < 0 || x->timing) ? 0 : gb;
     // eta window: a captured batch starts with a fold and spans whole windows
     if (x->batch > 0 && P.win) x->batch = (int)round_up(x->batch, P.win - 1);
@@ -481,7 +486,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
     advance_window(x, fold);
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, p0, p1));
-    if (x->opts.nranks > 1) {
+    if (x->use_comm) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
         NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
                                x->stream));
@@ -498,6 +503,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
 
 int build_graph(spx_ctx* x) {
     if (x->graph_exec || x->batch <= 0) return SPX_OK;
+    if (x->use_comm && !x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
     HIP_TRY(hipStreamBeginCapture(x->stream, hipStreamCaptureModeThreadLocal));
     int rc = SPX_OK;
     const int nw_keep = x->nw;
@@ -506,10 +512,21 @@ int build_graph(spx_ctx* x) {
     x->nw = nw_keep;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(x->stream, &g);
+    hipError_t ei = hipSuccess;
+    if (rc == SPX_OK && e == hipSuccess) ei = hipGraphInstantiate(&x->graph_exec, g, nullptr, nullptr, 0);
+    if (x->use_comm && (rc != SPX_OK || e != hipSuccess || ei != hipSuccess)) {
+        // RCCL calls that cannot be captured: launch the passes eagerly
+        if (g) (void)hipGraphDestroy(g);
+        x->graph_exec = nullptr;
+        x->batch = 0;
+        x->graph_fallback = true;
+        (void)hipGetLastError();
+        return SPX_OK;
+    }
     if (rc != SPX_OK) return rc;
     if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
     x->graph = g;
-    HIP_TRY(hipGraphInstantiate(&x->graph_exec, g, nullptr, nullptr, 0));
+    if (ei != hipSuccess) return fail(SPX_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
     // the first launch of a fresh graph pays its upload (measured 13 ms for a
     // 63-node graph): do it here, not inside somebody's timed loop
     HIP_TRY(hipGraphUpload(x->graph_exec, x->stream));
@@ -767,7 +784,7 @@ int reinvert_current(spx_ctx* x) {
 
 int create_tail(spx_ctx* x) {
     SPX_TRY(do_reset(x));
-    if (x->opts.nranks == 1 && !x->persist) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
+    if (!x->use_comm && !x->persist) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
     return SPX_OK;
 }
 
@@ -857,7 +874,7 @@ int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]) {
 
 int spx_attach_comm(spx_ctx* x, const uint8_t id[SPX_COMM_ID_BYTES]) {
     if (!x || !id) return fail(SPX_ERR_ARG, "NULL argument");
-    if (x->opts.nranks == 1) return SPX_OK;
+    if (!x->use_comm) return SPX_OK;
     if (x->comm_ready) return fail(SPX_ERR_STATE, "communicator already attached");
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
@@ -1121,7 +1138,7 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
     const int ps = x->P.pr_stride;
-    if (x->opts.nranks > 1) {
+    if (x->use_comm) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
         NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * ps, ncclUint8, x->comm, x->stream));
     }

@@ -1,0 +1,40 @@
+"""GPU: the RCCL MINLOC path on one GPU (SPX_FLAG_COMM1: a one-rank
+communicator, so ncclAllGather runs exactly as in the multi-GPU bench),
+eager and captured into hipGraphs, against the plain single-rank loop —
+bit-identical (a one-rank all-gather is a copy)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("window", [-1, 16])
+@pytest.mark.parametrize("graph_batch", [-1, 16])
+def test_comm1_matches_single_rank(spx, window, graph_batch):
+    m, n, seed, k = 300, 1200, 3, 150
+    with spx.Context(m=m, n=n, seed=seed, window=window, persist=False) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+    with spx.Context(m=m, n=n, seed=seed, window=window, comm1=True, graph_batch=graph_batch) as ctx:
+        ctx.attach_comm(spx.comm_unique_id())
+        st, piv = ctx.iterate(k)
+        cfg = ctx.config()
+        s = ctx.state(binv=True)
+        p, e, opt = ctx.price()
+        q, st2 = ctx.pivot()
+    assert piv == k
+    if graph_batch > 0:
+        assert cfg["graph_batch"] in (0, 16 if window < 0 else 30)  # 0: capture fell back to eager
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(s[key], rs[key]), key
+
+
+def test_comm1_graph_capture_used(spx):
+    """Report whether RCCL accepted the capture (the multi-GPU bench relies on it
+    for launch-free passes; a refusal falls back to eager launches)."""
+    with spx.Context(m=256, n=1024, seed=0, window=-1, comm1=True) as ctx:
+        ctx.attach_comm(spx.comm_unique_id())
+        ctx.iterate(40)
+        cfg = ctx.config()
+    print(f"RCCL capture: graph_batch={cfg['graph_batch']}")
+    assert cfg["graph_batch"] in (0, 16)
