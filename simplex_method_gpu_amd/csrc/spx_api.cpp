@@ -104,6 +104,7 @@ struct spx_ctx {
     bool comm_ready = false;
     bool use_comm = false;  // MINLOC through RCCL: nranks > 1, or SPX_FLAG_COMM1 (one-rank test of that path)
     bool graph_fallback = false;  // a capture with RCCL calls failed: eager passes
+    bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
 
     // graph replay of `batch` passes
     hipGraphExec_t graph_exec = nullptr;
@@ -414,6 +415,12 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         x->rs_recv = rb;
     }
     x->use_comm = G > 1 || (x->opts.flags & SPX_FLAG_COMM1);
+    P.price_grid = pc.grid;
+    P.defer_price = 0;  // set per launch by enqueue_pass (the step-wise API keeps the tail)
+    // measured at C3: window mode 107.0 -> 105.8 us per pass (the B_w rows are
+    // already in flight when k_update reduces the partials); explicit mode
+    // 126.5 -> 128.5 us (its stream waits for the reduction), so window only
+    x->defer_ok = P.win && !x->use_comm && !P.split_tail && !P.row_shard && !(x->opts.flags & SPX_FLAG_STAMPS);
     P.price_out = x->send;
     P.price_in = x->use_comm ? x->recv : x->send;
     P.nin = G;
@@ -485,14 +492,16 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     const bool fold = fold_due(x);
     if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
     advance_window(x, fold);
-    HIP_TRY(launch_price(x->P, x->pcfg, x->stream, p0, p1));
+    Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
+    Pp.defer_price = x->defer_ok ? 1 : 0;
+    HIP_TRY(launch_price(Pp, x->pcfg, x->stream, p0, p1));
     if (x->use_comm) {
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
         NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
                                x->stream));
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
-    HIP_TRY(launch_update(x->P, x->ucfg, x->stream, u0, u1));
+    HIP_TRY(launch_update(Pp, x->ucfg, x->stream, u0, u1));
     if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
     if (x->P.row_shard) {  // ratio-test all-gather (header + candidate row), then finalise
         NCCL_TRY(ncclAllGather(x->P.rs_send, x->rs_recv, (size_t)x->P.rs_stride, ncclUint8, x->comm, x->stream));

@@ -190,6 +190,11 @@ struct Params {
     double feas_tol;
     double* W;             // Devex reference weights (n)
     double* dvx_e;         // Devex: reduced cost of the chosen column (k_price -> k_update)
+    // deferred pricing tail (one rank, captured/eager passes): k_price stores
+    // its workgroup partials and returns; every k_update workgroup reduces the
+    // price_grid partials itself (no last-workgroup fan-in, no ticket)
+    int32_t defer_price;
+    int32_t price_grid;
 };
 
 // Optimality test on the merged entering candidate (v4:299-302): the reduced

@@ -46,7 +46,7 @@ namespace spx {
 #define SPX_WIN_APLDS 0  // eta-window FTRAN: A_p from LDS (1) or through L1/L2 (0)
 #endif
 #ifndef SPX_WIN_U1
-#define SPX_WIN_U1 16  // eta-window FTRAN stream, 1 row per wave: dbl2 loads per lane per round trip
+#define SPX_WIN_U1 8  // eta-window FTRAN stream, 1 row per wave: dbl2 loads per lane per round trip
 #endif
 bool kernels_inplace() { return SPX_INPLACE != 0; }
 
@@ -348,6 +348,15 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
     if (lane == 0) red[wave] = PricePartial{best, bj, bw, be};
     __syncthreads();
+    if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
+        if (tid == 0) {
+            PricePartial w = red[0];
+            for (int i = 1; i < WAVES; ++i)
+                if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
+            P.price_partials[blockIdx.x] = w;
+        }
+        return;
+    }
     if (tid == 0) {
         PricePartial w = red[0];
         for (int i = 1; i < WAVES; ++i)
@@ -482,10 +491,12 @@ struct TailPre {
     double c_p;
     int32_t cnt, kp, last;
     double wp;  // Devex: the entering column's weight
+    bool has_e;
+    double e_enter;  // deferred pricing tail: the entering column's reduced cost
 };
 
 __device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState* st, int64_t p) {
-    TailPre t{false, 0.0, 0, -1, -1, 0.0};
+    TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
     if (p < 0 || p >= P.n) return t;
     t.c_p = P.c[p];
     t.cnt = st->nb_count;
@@ -534,7 +545,7 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
     }
     st->p = p;
     st->q = q;
-    st->min_e = P.devex ? *P.dvx_e : min_e;
+    st->min_e = min_e;  // the entering reduced cost (callers resolve Devex's key)
     st->iter = it + 1;
 }
 
@@ -561,7 +572,8 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
         return;
     }
     const double c_p = pre ? pre->c_p : P.c[p];
-    pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, c_p), min_e, it, pre);
+    const double e_rep = !P.devex ? min_e : (pre && pre->has_e ? pre->e_enter : *P.dvx_e);
+    pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, c_p), e_rep, it, pre);
     st_agent(&st->ticket_update, 0u);
     tail_mark(P, 1, tm);
 }
@@ -574,8 +586,22 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
 // loads of B per lane per round trip.  a: A_p in global memory or in LDS.
 template <int U, int R>
 __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2* __restrict__ src, int64_t base,
-                                         int64_t L2, int lane, double (&acc)[R]) {
+                                         int64_t L2, int lane, double (&acc)[R], const dbl2 (*pre)[R] = nullptr) {
     int64_t k = lane;
+    if (pre) {  // the first U chunks were loaded at kernel entry
+        dbl2 av[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) av[t] = a[k + t * 64];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                acc[u] = fma(pre[t][u].x, av[t].x, acc[u]);
+                acc[u] = fma(pre[t][u].y, av[t].y, acc[u]);
+            }
+        }
+        k += U * 64;
+    }
     for (; k + (U - 1) * 64 < L2; k += U * 64) {
         dbl2 av[U], bv[U][R];
 #pragma unroll
@@ -607,28 +633,70 @@ __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2*
 template <int BLOCK, int R, bool RS, bool WIN>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
-    if (stopped(st)) return;
-    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
-    stamp_start(slot);
     using Lds = UpdLds<BLOCK>;
     constexpr int WAVES = BLOCK / 64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // eta window: B_w is read-only, so this wave's rows can be in flight
+    // before anything else is known (status, entering column, pivot state);
+    // a short-lived wave otherwise starts its stream after that chain of
+    // dependent loads (tools/stream_bench.hip: the bare 134 MB one-shot
+    // stream takes 23 us)
+    constexpr int PFU = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
+    dbl2 pfb[PFU][R];
+    const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
+    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    if (pf_ok) {
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + pf_row * (P.L >> 1);
+#pragma unroll
+        for (int t = 0; t < PFU; ++t)
+#pragma unroll
+            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<SPX_NT_BLOAD>(&b0[u * (P.L >> 1) + lane + t * 64]);
+    }
+    if (stopped(st)) return;
+    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
+    stamp_start(slot);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-    // entering column: MINLOC over all ranks' candidates (v4:294-302)
-    double min_e = INFINITY;
+    // entering column: MINLOC over all ranks' candidates (v4:294-302), or,
+    // with the pricing tail deferred, over k_price's workgroup partials
+    // (every workgroup the same reduction: the same winner)
+    double min_e = INFINITY, e_enter = 0.0;
     int64_t p = INT64_MAX;
     int gw = 0;
-    for (int g = 0; g < P.nin; ++g) {
-        const ArgMinEntry e = P.price_in[g * P.pr_stride];
-        if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
+    if (P.defer_price) {
+        PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
+        for (int g = tid; g < P.price_grid; g += BLOCK) {
+            const PricePartial v = P.price_partials[g];
+            if (argmin_better(v.val, v.idx, w.val, w.idx)) w = v;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double v = __shfl_xor(w.val, off, 64);
+            const int64_t i = __shfl_xor(w.idx, off, 64);
+            const double pe = __shfl_xor(w.pad, off, 64);
+            if (argmin_better(v, i, w.val, w.idx)) { w.val = v; w.idx = i; w.pad = pe; }
+        }
+        __shared__ PricePartial s_pw[WAVES];
+        if (lane == 0) s_pw[wave] = w;
+        __syncthreads();
+        PricePartial t = s_pw[0];
+        for (int i = 1; i < WAVES; ++i)
+            if (argmin_better(s_pw[i].val, s_pw[i].idx, t.val, t.idx)) t = s_pw[i];
+        min_e = t.val;
+        p = t.idx;
+        e_enter = t.pad;
+    } else {
+        for (int g = 0; g < P.nin; ++g) {
+            const ArgMinEntry e = P.price_in[g * P.pr_stride];
+            if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
+        }
     }
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
-            st->min_e = min_e;
+            st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
             st->status = ST_OPTIMAL;
         }
         return;
@@ -682,8 +750,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
     for (int u = 0; u < R; ++u)
         ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
-    TailPre tpre{false, 0.0, 0, -1, -1, 0.0};
+    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
     if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st, p);
+    if (P.defer_price) {
+        tpre.has_e = true;
+        tpre.e_enter = e_enter;
+    }
     const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
@@ -726,10 +798,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
+            static_assert(U == PFU, "prefetch and stream chunking agree");
             if (SPX_WIN_APLDS && aplds)
-                win_rows<U, R>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc);
+                win_rows<U, R>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc,
+                               pf_ok ? pfb : nullptr);
             else
-                win_rows<U, R>(ap, src, base, L2, lane, acc);
+                win_rows<U, R>(ap, src, base, L2, lane, acc, pf_ok ? pfb : nullptr);
         } else if (nvalid > 0) {
             for (int64_t k = lane; k < L2; k += 64) {
                 const dbl2 av = ap[k];
@@ -972,7 +1046,7 @@ __device__ void harris_tail(const Params& P, DevState* st, int64_t p, double min
         if (argmin_better(wr[k].val, wr[k].idx, w.val, w.idx)) w = wr[k];
     const int64_t q = w.idx;  // exists: pass 1's winner satisfies the bound
     const double aq = a_new[q], cbq = P.c_B[q];
-    pivot_bookkeeping(P, st, p, q, P.b_ixs[q], aq, y_scalar(t.T, aq, cbq, P.c[p]), min_e, it);
+    pivot_bookkeeping(P, st, p, q, P.b_ixs[q], aq, y_scalar(t.T, aq, cbq, P.c[p]), P.devex ? *P.dvx_e : min_e, it);
 }
 
 // The pivot tail as its own one-workgroup launch (split_tail): the k_update
