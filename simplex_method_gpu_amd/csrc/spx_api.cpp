@@ -417,10 +417,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     x->use_comm = G > 1 || (x->opts.flags & SPX_FLAG_COMM1);
     P.price_grid = pc.grid;
     P.defer_price = 0;  // set per launch by enqueue_pass (the step-wise API keeps the tail)
-    // measured at C3: window mode 107.0 -> 105.8 us per pass (the B_w rows are
-    // already in flight when k_update reduces the partials); explicit mode
-    // 126.5 -> 128.5 us (its stream waits for the reduction), so window only
-    x->defer_ok = P.win && !x->use_comm && !P.split_tail && !P.row_shard && !(x->opts.flags & SPX_FLAG_STAMPS);
+    // measured: C3 window 107.0 -> 105.8 us per pass (the B_w rows are already
+    // in flight when k_update reduces the partials), C2 explicit 24.9 -> 23.2
+    // us; C3 explicit 126.5 -> 128.5 us (its stream waits for the reduction),
+    // so not for large explicit passes
+    x->defer_ok = (P.win || m <= 2048) && !x->use_comm && !P.split_tail && !P.row_shard && !(x->opts.flags & SPX_FLAG_STAMPS);
     P.price_out = x->send;
     P.price_in = x->use_comm ? x->recv : x->send;
     P.nin = G;

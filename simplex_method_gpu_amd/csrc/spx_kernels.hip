@@ -643,7 +643,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // a short-lived wave otherwise starts its stream after that chain of
     // dependent loads (tools/stream_bench.hip: the bare 134 MB one-shot
     // stream takes 23 us)
-    constexpr int PFU = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
+    // (the explicit in-place update measured slower with its old rows loaded
+    // this way: C3 59 -> 66 us, so window only)
+    constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
     const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
@@ -826,7 +828,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         if (upd_x) sxa = sxw;
     } else if (nvalid == R) {
         constexpr int U = (R >= 4) ? 2 : 4;
+        static_assert(WIN || U == PFU, "prefetch and stream chunking agree");
         int64_t k = lane;
+        bool first = pf_ok;
         for (; k + (U - 1) * 64 < L2; k += U * 64) {
             dbl2 rv[U], av[U], bb[U], bv[U][R];
 #pragma unroll
@@ -835,8 +839,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 av[t] = ap[k + t * 64];
                 bb[t] = bp[k + t * 64];
 #pragma unroll
-                for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
+                for (int u = 0; u < R; ++u)
+                    bv[t][u] = first ? pfb[t < PFU ? t : 0][u] : ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
             }
+            first = false;
 #pragma unroll
             for (int t = 0; t < U; ++t) {
                 sxa = fma(rv[t].x, bb[t].x, sxa);
