@@ -61,6 +61,9 @@ def parse():
                     help="B^-1 representation: 0 library default, -1 explicit rank-1 update, 8/16/32/64 eta window")
     ap.add_argument("--replicated", action="store_true",
                     help="N > 1: keep B^-1 replicated instead of row-sharded (SPX_FLAG_ROW_SHARD)")
+    ap.add_argument("--comm1", action="store_true",
+                    help="rehearsal on one GPU: run the multi-rank path (torch.distributed + RCCL "
+                         "MINLOC + row-sharded B^-1) with a one-rank communicator")
     a = ap.parse_args()
     m, n = CONFIGS[a.config or "C3"]
     a.m = a.m or m
@@ -79,7 +82,8 @@ def main():
     if world == 1 and args.gpus > 1:
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
-    if world > 1:
+    multi = world > 1 or args.comm1  # the multi-rank code path (RCCL exchange)
+    if multi:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import simplex_method_gpu_amd as spx
 
@@ -89,26 +93,27 @@ def main():
         ctx = spx.Context(m=m, n=n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
                           update_rows=args.update_rows, update_block=args.update_block,
                           price_block=args.price_block, graph_batch=args.graph_batch,
-                          row_shard=(world > 1 and not args.replicated), window=args.window)
-        if world > 1:
+                          row_shard=(multi and not args.replicated), window=args.window,
+                          comm1=(args.comm1 and world == 1))
+        if multi:
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             ctx.attach_comm(obj[0])
         return ctx
 
     def barrier():
-        if world > 1:
+        if multi:
             dist.barrier()
 
     def reduce_max(vals):
-        if world == 1:
+        if not multi:
             return list(vals)
         t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.tolist()
 
     def reduce_sum(vals):
-        if world == 1:
+        if not multi:
             return list(vals)
         t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -158,7 +163,7 @@ def main():
 
     if piv_g > 0 and dt_g / piv_g <= dt_e / max(piv_e, 1):
         best_dt, best_piv = dt_g, piv_g
-        mode = ("hipGraph replay" if world == 1 else
+        mode = ("hipGraph replay" if not multi else
                 ("hipGraph replay incl. RCCL all-gathers" if cfg.get("graph_batch", 0) > 0 else
                  "eager + RCCL all-gather"))
     else:
@@ -222,7 +227,7 @@ def main():
                 "parallelism": ((f"pricing column-sharded x{world} (RCCL all-gather MINLOC), " +
                                  ("B^-1 replicated" if args.replicated else
                                   "B^-1 row-sharded (pivot row in a 2nd all-gather)"))
-                                if world > 1 else "single GPU"),
+                                if multi else "single GPU"),
                 "dispatch": mode,
             },
             "roofline": {
@@ -256,7 +261,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

@@ -248,7 +248,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.eps = x->opts.eps;
     // row shard of B^-1 (SPX_FLAG_ROW_SHARD with nranks > 1): rows
     // [r0, r0 + mloc), ping-pong storage; otherwise all rows, in place
-    P.row_shard = (G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD)) ? 1 : 0;
+    // (SPX_FLAG_COMM1: the row-sharded RCCL path with one rank, for tests)
+    P.row_shard = ((G > 1 || (x->opts.flags & SPX_FLAG_COMM1)) && (x->opts.flags & SPX_FLAG_ROW_SHARD)) ? 1 : 0;
     // leaving-row rule (SPX_RATIO_*); Harris runs its second pass in k_tail
     const int rule = x->opts.ratio_test;
     if (rule != SPX_RATIO_REFERENCE && rule != SPX_RATIO_GUARDED && rule != SPX_RATIO_HARRIS)

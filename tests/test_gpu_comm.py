@@ -38,3 +38,28 @@ def test_comm1_graph_capture_used(spx):
         cfg = ctx.config()
     print(f"RCCL capture: graph_batch={cfg['graph_batch']}")
     assert cfg["graph_batch"] in (0, 16)
+
+
+@pytest.mark.parametrize("graph_batch", [-1, 16])
+def test_comm1_row_shard_matches_single_rank(spx, oracle, graph_batch):
+    """The multi-GPU bench's default (row-sharded B^-1, two all-gathers per
+    pass, k_finalize_rs) through RCCL on one rank: same pivots as the single
+    rank, values within 1e-9 (the sharded s_y is reassociated), the optimum
+    of the oracle."""
+    m, n, seed, k = 300, 1200, 3, 150
+    with spx.Context(m=m, n=n, seed=seed, window=-1) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+    with spx.Context(m=m, n=n, seed=seed, window=-1, comm1=True, row_shard=True, graph_batch=graph_batch) as ctx:
+        ctx.attach_comm(spx.comm_unique_id())
+        st, piv = ctx.iterate(k)
+        s = ctx.state(binv=True)
+        r = ctx.solve()
+    assert piv == k and np.array_equal(s["b_ixs"], rs["b_ixs"])
+    for key in ("x_b", "y", "binv"):
+        a, b = s[key], rs[key]
+        assert np.max(np.abs(a - b)) <= 1e-9 * max(1.0, np.max(np.abs(b))), key
+    A, b, c = oracle.generate(m, n, seed)
+    o = oracle.solve(A, b, c, eps=1e-7)
+    assert r.status == spx.SolveStatus.OptimumFound and r.pivots == o.pivots
+    assert abs(r.z - o.z) <= 1e-9 * abs(o.z)
