@@ -16,7 +16,7 @@ GLPKDRV   := solver_glpk
 
 all: $(LIB) $(CLI) $(GLPKDRV) oracle
 
-$(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
+$(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_tableau.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -24,15 +24,19 @@ $(BUILD)/spx_reinv.o: $(SRC)/spx_reinv.hip $(SRC)/spx_reinv.h $(SRC)/spx_device.
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BUILD)/spx_tableau.o: $(SRC)/spx_tableau.hip $(SRC)/spx_tableau.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/spx_loop.o: $(SRC)/spx_loop.hip $(SRC)/spx_loop.h $(SRC)/spx_device.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/spx_api.o: $(SRC)/spx_api.cpp $(SRC)/spx_loop.h $(SRC)/spx_kernels.h $(SRC)/spx_reinv.h $(SRC)/spx_device.h include/simplex.h
+$(BUILD)/spx_api.o: $(SRC)/spx_api.cpp $(SRC)/spx_loop.h $(SRC)/spx_kernels.h $(SRC)/spx_reinv.h $(SRC)/spx_tableau.h $(SRC)/spx_device.h include/simplex.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o
+$(LIB): $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDFLAGS)
 
 $(CLI): $(SRC)/solver_main.cpp $(SRC)/lp_io.cpp $(SRC)/lp_io.h $(SRC)/mps_io.cpp $(SRC)/mps_io.h include/simplex.h $(LIB)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 3
+#define SPX_ABI_VERSION 4
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -144,6 +144,13 @@ typedef struct spx_opts {
                               RCCL anyway (spx_attach_comm with a one-rank id), so
                               the communicator path, graph-captured RCCL calls
                               included, can be checked on one GPU            */
+#define SPX_FLAG_TABLEAU 256 /* window tableau: with the eta window,
+                                also keep T_w = B_w A and dw = y_w A - c in HBM and
+                                fold them with B_w (fp64 MFMA), so a pass reads no
+                                A column and no B_w row: pricing reads T_w[q, j],
+                                dw[j] and the window row of each non-basic column,
+                                FTRAN the column T_w[:, p].  Needs the window (0 =
+                                auto selects 64) and one rank; twice A's memory. */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass
@@ -281,8 +288,9 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * in global, 1 y in LDS, 2 y and the window base row in LDS), [4] update
  * threads per workgroup, [5] update rows per wave, [6] update workgroups,
  * [7] passes per captured hipGraph (0 = eager), [8] persistent loop kernel
- * in use (1) or not (0), [9] its threads per workgroup. */
-#define SPX_CONFIG_FIELDS 10
+ * in use (1) or not (0), [9] its threads per workgroup, [10] window tableau
+ * (SPX_FLAG_TABLEAU) in use. */
+#define SPX_CONFIG_FIELDS 11
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:

@@ -22,6 +22,7 @@
 #include "spx_device.h"
 #include "spx_kernels.h"
 #include "spx_reinv.h"
+#include "spx_tableau.h"
 #include "spx_loop.h"
 
 using namespace spx;
@@ -308,6 +309,14 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         SPX_TRY(x->alloc(&P.W, (size_t)n));
         SPX_TRY(x->alloc(&P.dvx_e, 1));
     }
+    // window tableau: T_w = B_w A and dw = y_w A - c beside the eta window
+    P.tab = (x->opts.flags & SPX_FLAG_TABLEAU) ? 1 : 0;
+    if (P.tab) {
+        if (G > 1 || P.row_shard || (x->opts.flags & SPX_FLAG_COMM1))
+            return fail(SPX_ERR_ARG, "the window tableau runs on one rank");
+        if (x->opts.window < 0) return fail(SPX_ERR_ARG, "the window tableau needs the eta window (window > 0 or 0 = auto)");
+        if (x->opts.window == 0) KW = 64;
+    }
     if (KW > 0 && P.row_shard) return fail(SPX_ERR_ARG, "the eta window needs replicated B^-1 (no row sharding)");
     if (KW > 0 && !(KW == 8 || KW == 16 || KW == 32 || KW == 64))
         return fail(SPX_ERR_ARG, "window must be 8, 16, 32 or 64 (got %d)", KW);
@@ -320,6 +329,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         SPX_TRY(x->alloc(&P.Urows, (size_t)(KW * KW)));
         SPX_TRY(x->alloc(&P.SY, (size_t)KW));
         SPX_TRY(x->alloc(&P.xw, (size_t)L));
+    }
+    if (P.tab) {
+        SPX_TRY(x->alloc(&P.T, (size_t)(L * n)));
+        SPX_TRY(x->alloc(&P.dw, (size_t)n));
     }
     P.pr_stride = P.win ? 1 + P.win / 2 : 1;
 
@@ -341,9 +354,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         pc.block = ybytes <= 72 * 1024 ? 512 : 1024;
     const size_t red_bytes = (size_t)(pc.block / 64) * sizeof(PricePartial) + 16;
     const size_t lds_cap = 150 * 1024;
-    pc.lds_y = ybytes + red_bytes <= lds_cap && !(x->opts.flags & SPX_FLAG_GLOBAL_Y);
-    // eta window: the pending base row next to y when both fit
-    pc.wm = !P.win ? 0 : ((pc.lds_y && 2 * ybytes + red_bytes <= lds_cap) ? 1 : 2);
+    pc.lds_y = ybytes + red_bytes <= lds_cap && !(x->opts.flags & SPX_FLAG_GLOBAL_Y) && !P.tab;
+    // eta window: the pending base row next to y when both fit; the tableau
+    // pass stages nothing (wm 3)
+    pc.wm = P.tab ? 3 : (!P.win ? 0 : ((pc.lds_y && 2 * ybytes + red_bytes <= lds_cap) ? 1 : 2));
     pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (pc.wm == 1 ? ybytes : 0) + red_bytes;
     int per_cu = 0;
     HIP_TRY(price_prepare(pc, &per_cu));
@@ -384,7 +398,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
     // the persistent loop kernel replaces the two-kernel pass where it applies
-    if (P.win && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
+    if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
         x->lcfg.block = x->opts.loop_block;
         HIP_TRY(loop_prepare(P, x->cus, x->lcfg));
@@ -437,6 +451,19 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     return SPX_OK;
 }
 
+// Window tableau: T_w = B_w A and dw = y_w A - c from the current state (no
+// pivot pending).  At the slack basis B_w = I, so T_w is a copy of A.
+int tab_rebuild(spx_ctx* x, bool slack) {
+    if (!x->P.tab) return SPX_OK;
+    if (slack)
+        HIP_TRY(hipMemcpyAsync(x->P.T, x->A, (size_t)(x->L * x->n) * sizeof(double), hipMemcpyDeviceToDevice,
+                               x->stream));
+    else
+        HIP_TRY(launch_tab_build(x->P, x->stream));
+    HIP_TRY(launch_reduced_costs(x->P, x->P.dw, x->stream));
+    return SPX_OK;
+}
+
 int do_reset(spx_ctx* x) {
     const size_t mb = (size_t)(std::max<int64_t>(x->P.mloc, 1) * x->L) * sizeof(double);
     HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
@@ -444,6 +471,7 @@ int do_reset(spx_ctx* x) {
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
     HIP_TRY(launch_reset(x->P, x->stream));
+    SPX_TRY(tab_rebuild(x, true));
     HIP_TRY(hipStreamSynchronize(x->stream));
     x->pivots = 0;
     x->status = SPX_STATUS_MAX_ITER;
@@ -767,6 +795,7 @@ int reinvert_basis(spx_ctx* x, const int64_t* basis) {
         return fail(SPX_ERR_SINGULAR, "singular basis: no pivot above tolerance for column %lld (basis position %lld)",
                     (long long)basis[rs.bad_pos], (long long)rs.bad_pos);
     HIP_TRY(rv_launch_finish(x->P, R, x->rv_Ypart, x->stream));
+    SPX_TRY(tab_rebuild(x, false));
     x->nw = 0;
     return read_state(x);
 }
@@ -1296,6 +1325,7 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[7] = x->batch;
     out[8] = x->persist ? 1 : 0;
     out[9] = x->persist ? x->lcfg.block : 0;
+    out[10] = x->P.tab;
     return SPX_OK;
 }
 

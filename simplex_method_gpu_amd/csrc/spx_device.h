@@ -42,6 +42,11 @@
 //          Wt[j][tau] - c_j; alpha = B_w A_p + sum U[:,tau] Wt[p][tau];
 //   Qrows/Urows  the base rows B_w[q_tau,:] and coefficients U[q_tau][s<tau]
 //          (staged by k_price) from which k_fold rebuilds the r_tau.
+// Window tableau (tab = 1): with T_w = B_w A and dw = y_w A - c kept in HBM,
+//   r_tau . A_j = T_w[q_tau, j] + sum_{s<tau} U[q_tau][s] Wt[j][s],
+//   e_j = dw[j] + sum_tau SY[tau] Wt[j][tau],
+//   alpha = T_w[:, p] + sum_tau U[:, tau] Wt[p][tau];
+// the fold adds T_w += U Wt^T and dw += SY Wt^T (k_tab_fold, fp64 MFMA).
 // When nw reaches KW, k_fold folds the nw-1 complete pivots into B_w and y_w
 // (rank-(KW-1) update, read + write of B once) and the pending pivot becomes
 // tau = 0.
@@ -195,6 +200,14 @@ struct Params {
     // price_grid partials itself (no last-workgroup fan-in, no ticket)
     int32_t defer_price;
     int32_t price_grid;
+    // window tableau (SPX_FLAG_TABLEAU): T_w = B_w A (L x n,
+    // column-major like A) and dw = y_w A - c (n), both folded with B_w, so a
+    // pass reads T_w[q_tau, j], dw[j] and Wt[j][.] per column instead of A_j,
+    // and FTRAN reads the column T_w[:, p] instead of streaming B_w
+    int32_t tab;
+    int32_t pad_t;
+    double* T;
+    double* dw;
 };
 
 // Optimality test on the merged entering candidate (v4:299-302): the reduced

@@ -31,6 +31,7 @@
 #include "spx_common.h"
 #include "spx_fold.h"
 #include "spx_kernels.h"
+#include "spx_tableau.h"
 
 namespace spx {
 
@@ -99,7 +100,8 @@ __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, 
 // ---------------------------------------------------------------------------
 // WM: 0 = explicit B^-1 (y updated in the LDS fill); 1 = eta window with the
 // pending base row in LDS next to y; 2 = eta window, base row read from global
-// (L2) when y and the row do not both fit.
+// (L2) when y and the row do not both fit; 3 = window tableau (P.tab): no A
+// stream, each column reads T_w[q_tau, j], dw[j] and its Wt row.
 template <int BLOCK, bool LDS_Y, int WM>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // the first CH chunks of the first column stay in flight during the y
     // staging below (the A stream does not wait for the LDS fill)
     constexpr int CH = 8;
-    const bool pre = idx0 < nb && L2 >= CH * 64;
+    const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
     dbl2 v0[CH];
     if (pre) {
         const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
@@ -229,6 +231,68 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     stamp_stream(win, true);
     const int nlist = nb;
     const int stride = gridDim.x * WAVES;
+    // candidate update shared by every mode: Devex key, then the argmin
+    auto consider = [&](int64_t j, double e, double wn) {
+        double key = e;
+        if (WIN && P.devex) {
+            // Devex (include/simplex.h SPX_PRICING_DEVEX): the pending pivot's
+            // row entry wn = r.A_j updates this column's reference weight
+            double w = P.W[j];
+            if (pend) {
+                if (j == dvx_leave) w = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
+                else {
+                    const double g = wn / dvx_aq;
+                    w = fmax(w, g * g * dvx_wp);
+                }
+                if (lane == 0) P.W[j] = w;
+            }
+            key = (e < -P.eps) ? -(e * e) / w : INFINITY;
+        }
+        if (argmin_better(key, j, best, bj)) { best = key; bj = j; bw = wn; be = e; }
+    };
+    if constexpr (WM == 3) {
+        // window tableau: TPC columns per wave in flight; lane s < tau holds
+        // Wt[j][s]; r_tau.A_j = T_w[q,j] + sum_s U[q][s] Wt[j][s] and
+        // e_j = dw[j] + sum_s SY[s] Wt[j][s] + SY[tau] r_tau.A_j
+        constexpr int TPC = 4;
+        const int64_t qq = pend ? st->q : 0;
+        for (int idx = idx0; idx < nlist; idx += stride * TPC) {
+            int64_t jj[TPC];
+            double wv[TPC], tq[TPC], dv[TPC], sa[TPC], wn[TPC];
+#pragma unroll
+            for (int c = 0; c < TPC; ++c) {
+                const int ic = idx + c * stride;
+                jj[c] = ic < nlist ? (int64_t)P.nb_list[ic] : -1;
+            }
+#pragma unroll
+            for (int c = 0; c < TPC; ++c) {
+                const int64_t j = jj[c] < 0 ? 0 : jj[c];
+                wv[c] = (pend && lane < tau) ? P.Wt[j * KW + lane] : 0.0;
+                tq[c] = pend ? P.T[j * L + qq] : 0.0;
+                dv[c] = P.dw[j];
+                sa[c] = syl * wv[c];
+                wn[c] = uq * wv[c];
+            }
+            if (pend) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+                    for (int c = 0; c < TPC; ++c) {
+                        const double ta = __shfl_xor(sa[c], off, 64);
+                        const double tb = __shfl_xor(wn[c], off, 64);
+                        sa[c] += ta;
+                        wn[c] += tb;
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < TPC; ++c) {
+                if (jj[c] < 0) continue;
+                const double w = tq[c] + wn[c];
+                if (pend && lane == 0) P.Wt[jj[c] * KW + tau] = w;
+                consider(jj[c], pend ? fma(syp, w, dv[c] + sa[c]) : dv[c], w);
+            }
+        }
+    } else {
     // The first CH chunks of every column are loaded before the previous
     // column's reduction (and, for the first column, before the LDS fill), so
     // a wave's A stream does not stall at column boundaries.
@@ -314,7 +378,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&cn[lane + u * 64]);
         }
-        double e, wn = 0.0, key;
+        double e, wn = 0.0;
         if (WIN && pend) {
             // r_tau . A_j = B_w[q,:] . A_j + sum_s U[q][s] Wt[j][s]; the window
             // terms join the lane partials before the butterflies
@@ -326,22 +390,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         } else {
             e = wave_sum(a0 + a1) - P.c[j];
         }
-        key = e;
-        if (WIN && P.devex) {
-            // Devex (include/simplex.h SPX_PRICING_DEVEX): the pending pivot's
-            // row entry wn = r.A_j updates this column's reference weight
-            double w = P.W[j];
-            if (pend) {
-                if (j == dvx_leave) w = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
-                else {
-                    const double g = wn / dvx_aq;
-                    w = fmax(w, g * g * dvx_wp);
-                }
-                if (lane == 0) P.W[j] = w;
-            }
-            key = (e < -P.eps) ? -(e * e) / w : INFINITY;
-        }
-        if (argmin_better(key, j, best, bj)) { best = key; bj = j; bw = wn; be = e; }
+        consider(j, e, wn);
+    }
     }
 
     stamp_stream(win, false);
@@ -648,7 +698,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
-    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    const bool pf_ok = WIN && !RS && !P.tab && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
     if (pf_ok) {
         const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + pf_row * (P.L >> 1);
 #pragma unroll
@@ -791,13 +841,18 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
         // A_p staged in LDS once per workgroup (SPX_WIN_APLDS) instead of
         // every wave re-reading it through L1/L2 beside the B stream
-        const bool aplds = SPX_WIN_APLDS && L * 8 <= 65536;
+        const bool aplds = SPX_WIN_APLDS && L * 8 <= 65536 && !P.tab;
         if (SPX_WIN_APLDS && aplds) {
             dbl2* d = reinterpret_cast<dbl2*>(smem + Lds::bytes);
             for (int64_t kk = tid; kk < L2; kk += BLOCK) d[kk] = ap[kk];
             __syncthreads();
         }
-        if (nvalid == R) {
+        if (P.tab) {
+            // window tableau: B_w[i,:] . A_p is the stored T_w[i, p]
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (u < nvalid && lane == 0) acc[u] = P.T[p * L + gr0 + u];
+        } else if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
             static_assert(U == PFU, "prefetch and stream chunking agree");
@@ -1398,6 +1453,7 @@ static hipError_t price_dispatch(const PriceCfg& c, const Params* P, hipStream_t
         if (c.lds_y) SPX_PV(true, 2);
         SPX_PV(false, 2);
     }
+    if (c.wm == 3) SPX_PV(false, 3);
 #undef SPX_PV
     return hipErrorInvalidValue;
 }
@@ -1440,6 +1496,10 @@ static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipE
 }
 
 hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
+    if (P.tab) {  // T_w and dw first: k_fold resets the window
+        const hipError_t e = launch_tab_fold(P, min_nw, cus, s);
+        if (e != hipSuccess) return e;
+    }
     const int nx = (int)(P.L / 64);
     int64_t ny = ((int64_t)4 * cus + nx - 1) / nx;
     const int64_t maxy = (P.m + 63) / 64;  // at least one 16-row tile per wave

@@ -1,0 +1,17 @@
+// spx_tableau.h — host-side launchers of the window-tableau kernels
+// (spx_tableau.hip; SPX_FLAG_TABLEAU).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "spx_device.h"
+
+namespace spx {
+
+// T_w += U Wt^T and dw += SY Wt^T for the nw-1 complete pivots of the window
+// when nw >= min_nw (the same test as k_fold, which must run after it: k_fold
+// resets nw).  No-op unless P.tab.
+hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s);
+// T_w = B_w A (B_w = P.B0, row-major): after a reinversion or a warm start.
+hipError_t launch_tab_build(const Params& P, hipStream_t s);
+
+}  // namespace spx
