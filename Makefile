@@ -24,11 +24,11 @@ $(BUILD)/spx_reinv.o: $(SRC)/spx_reinv.hip $(SRC)/spx_reinv.h $(SRC)/spx_device.
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/spx_tableau.o: $(SRC)/spx_tableau.hip $(SRC)/spx_tableau.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
+$(BUILD)/spx_tableau.o: $(SRC)/spx_tableau.hip $(SRC)/spx_tableau.h $(SRC)/spx_grid.h $(SRC)/spx_loop.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/spx_loop.o: $(SRC)/spx_loop.hip $(SRC)/spx_loop.h $(SRC)/spx_device.h $(SRC)/spx_common.h
+$(BUILD)/spx_loop.o: $(SRC)/spx_loop.hip $(SRC)/spx_loop.h $(SRC)/spx_grid.h $(SRC)/spx_device.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

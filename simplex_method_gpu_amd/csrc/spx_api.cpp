@@ -371,6 +371,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (x->max_local_cols < 2LL * pc.grid * waves)
         pc.grid = (int)std::max<int64_t>(1, std::min<int64_t>(pc.grid, std::max<int64_t>(x->cus,
                                                                    x->max_local_cols / (2 * waves))));
+    // window tableau: a column is a few short loads (no stream); each wave
+    // keeps 4 columns in flight (k_price WM 3), so one pass over the list
+    if (P.tab) pc.grid = (int)std::max<int64_t>(1, std::min(cap, (x->max_local_cols + 4 * waves - 1) / (4 * waves)));
     if (x->opts.price_grid > 0) pc.grid = x->opts.price_grid;
 
     UpdateCfg& uc = x->ucfg;
@@ -407,6 +410,18 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         // (8.3k vs 9.3k it/s), so by default only then
         const bool want = (x->opts.flags & SPX_FLAG_PERSIST) || !x->lcfg.lds_r;
         if (x->lcfg.ok && want) {
+            SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
+            SPX_TRY(x->alloc(&x->la.up, (size_t)x->lcfg.grid));
+            SPX_TRY(x->alloc(&x->la.ls, 1));
+            SPX_TRY(x->alloc(&x->la.clock, (size_t)(3 * 64)));
+            x->persist = true;
+        }
+    }
+    // window tableau: the persistent tableau loop (k_tab_loop) unless told not to
+    if (P.tab && G == 1 && P.ratio != RATIO_HARRIS &&
+        !(x->opts.flags & (SPX_FLAG_STAMPS | SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
+        HIP_TRY(tab_loop_prepare(P, x->cus, x->lcfg));
+        if (x->lcfg.ok) {
             SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
             SPX_TRY(x->alloc(&x->la.up, (size_t)x->lcfg.grid));
             SPX_TRY(x->alloc(&x->la.ls, 1));
@@ -666,7 +681,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
             ++x->n_loop;
             HIP_TRY(hipEventRecord(e0, x->stream));
         }
-        HIP_TRY(launch_loop(x->P, a, x->lcfg, x->stream));
+        HIP_TRY(x->P.tab ? launch_tab_loop(x->P, a, x->lcfg, x->stream) : launch_loop(x->P, a, x->lcfg, x->stream));
         if (e1) HIP_TRY(hipEventRecord(e1, x->stream));
         if (x->timing) {  // phase split from workgroup 0's clock (s_memrealtime, 100 MHz)
             unsigned long long ck[3 * 64];

@@ -1261,6 +1261,10 @@ __global__ __launch_bounds__(1024) void k_flush(Params P) {
         const dbl2* r2 = reinterpret_cast<const dbl2*>(r);
         const double sy = P.win ? P.SY[0] : st->s_y;
         for (int64_t k = tid; k < L2; k += BLOCK) yout[k] = y_apply(sy, r2[k], yin[k]);
+        // window tableau: dw = y_w A - c follows y_w; the pending pivot is
+        // tau = 0 after the fold, so r.A_j = T_w[q, j]
+        if (P.tab)
+            for (int64_t j = tid; j < P.n; j += BLOCK) P.dw[j] = fma(sy, P.T[j * L + st->q], P.dw[j]);
     }
     if (upd_x) {
         // s_x exactly as k_update's row stream accumulates it (every wave alike)

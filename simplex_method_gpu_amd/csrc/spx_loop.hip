@@ -9,6 +9,7 @@
 
 #include "spx_common.h"
 #include "spx_loop.h"
+#include "spx_grid.h"
 
 namespace spx {
 
@@ -26,32 +27,6 @@ struct LoopLds {  // the small shared region after y_w (and the base row)
     UpdPartial uwin;    // the merged leaving candidate
     int64_t kp, lastv;  // list slots read in phase B for the pivot's list change
 };
-
-// Grid barrier: every wave drains its stores, workgroup barrier, one lane
-// adds to the counter and polls it (sc1) up to the target, workgroup barrier.
-// Bounded: returns false (and sets err) when the counter does not arrive.
-__device__ __forceinline__ bool grid_sync(LoopState* ls, uint32_t target, int* s_ok) {
-    drain_vmem();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        const uint32_t old = __hip_atomic_fetch_add(&ls->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 < target) {
-            uint32_t spins = 0;
-            while (ld_agent(&ls->bar) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 24) || ld_agent(&ls->err)) {
-                    st_agent(&ls->err, 1);
-                    ok = 0;
-                    break;
-                }
-            }
-        }
-        *s_ok = ok;
-    }
-    __syncthreads();
-    return *s_ok != 0;
-}
 
 __device__ __forceinline__ void price_merge(PricePartial& a, const PricePartial& b) {
     if (argmin_better(b.val, b.idx, a.val, a.idx)) a = b;

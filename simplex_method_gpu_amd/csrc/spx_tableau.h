@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "spx_device.h"
+#include "spx_loop.h"
 
 namespace spx {
 
@@ -13,5 +14,9 @@ namespace spx {
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s);
 // T_w = B_w A (B_w = P.B0, row-major): after a reinversion or a warm start.
 hipError_t launch_tab_build(const Params& P, hipStream_t s);
+// Persistent tableau loop (k_tab_loop): whole passes in one cooperative
+// launch, one workgroup per CU; ok = false when it cannot be used.
+hipError_t tab_loop_prepare(const Params& P, int cus, LoopCfg& c);
+hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s);
 
 }  // namespace spx

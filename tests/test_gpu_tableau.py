@@ -23,13 +23,16 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
+@pytest.mark.parametrize("persist", [False, True])
 @pytest.mark.parametrize("window", WINDOWS)
 @pytest.mark.parametrize("m,n,seed,k", [(257, 771, 2, 150), (1000, 3000, 3, 140), (64, 200, 5, 90)])
-def test_tableau_state_matches_oracle(spx, oracle, window, m, n, seed, k):
+def test_tableau_state_matches_oracle(spx, oracle, window, m, n, seed, k, persist):
+    """Two-kernel passes (k_price WM 3 + k_update) and the persistent tableau
+    loop (k_tab_loop) both follow the oracle."""
     A, b, c = oracle.generate(m, n, seed)
     ref = oracle.solve(A, b, c, max_iter=k, eps=1e-7, want_state=True, trace_cap=k)
-    with spx.Context(A, b, c, eps=1e-7, window=window, tableau=True) as ctx:
-        assert ctx.config()["tableau"] == 1 and ctx.config()["persistent"] == 0
+    with spx.Context(A, b, c, eps=1e-7, window=window, tableau=True, persist=persist) as ctx:
+        assert ctx.config()["tableau"] == 1 and ctx.config()["persistent"] == int(persist)
         st, piv = ctx.iterate(k)
         s = ctx.state(binv=True)
         e = ctx.reduced_costs()
@@ -78,16 +81,27 @@ def test_tableau_readback_mid_window_then_continue(spx, oracle):
 
 
 def test_tableau_graph_eager_bit_identical(spx):
+    """Two-kernel passes: graph replay, eager launches and every pricing
+    geometry give the same bits.  The persistent loop groups the ratio test's
+    c_B.alpha sum by its own geometry: same pivots, values within 1e-12."""
     m, n, seed, k = 300, 1200, 7, 160
     runs = []
     for kw in (dict(), dict(graph_batch=-1), dict(graph_batch=5), dict(price_grid=3), dict(price_block=1024)):
-        with spx.Context(m=m, n=n, seed=seed, window=32, tableau=True, **kw) as ctx:
+        with spx.Context(m=m, n=n, seed=seed, window=32, tableau=True, persist=False, **kw) as ctx:
+            assert ctx.config()["persistent"] == 0
             ctx.iterate(k)
             runs.append((kw, ctx.state(binv=True)))
     s0 = runs[0][1]
     for kw, s in runs[1:]:
         for key in ("b_ixs", "x_b", "y", "binv"):
             assert np.array_equal(s[key], s0[key]), (kw, key)
+    with spx.Context(m=m, n=n, seed=seed, window=32, tableau=True) as ctx:
+        assert ctx.config()["persistent"] == 1
+        st, piv = ctx.iterate(k)
+        s = ctx.state(binv=True)
+    assert piv == k and np.array_equal(s["b_ixs"], s0["b_ixs"])
+    for key in ("x_b", "y", "binv"):
+        assert _rel(s[key], s0[key]) <= 1e-12, key
 
 
 def test_tableau_matches_window(spx):
@@ -182,13 +196,15 @@ def test_tableau_devex_matches_window_devex(spx):
     """Devex weights come from the pass's r.A_j (Wt[j][tau]) in both modes."""
     m, n, seed, k = 300, 1200, 5, 150
     out = {}
-    for tab in (False, True):
+    for tab, persist in ((False, False), (True, False), (True, True)):
         with spx.Context(m=m, n=n, seed=seed, window=16, pricing=spx.PRICING_DEVEX, tableau=tab,
-                         persist=False) as ctx:
+                         persist=persist) as ctx:
             ctx.iterate(k)
-            out[tab] = ctx.state(binv=True)
-    assert np.array_equal(out[False]["b_ixs"], out[True]["b_ixs"])
-    assert _rel(out[True]["x_b"], out[False]["x_b"]) <= 1e-10
+            out[tab, persist] = ctx.state(binv=True)
+    ref = out[False, False]
+    for key in ((True, False), (True, True)):
+        assert np.array_equal(out[key]["b_ixs"], ref["b_ixs"]), key
+        assert _rel(out[key]["x_b"], ref["x_b"]) <= 1e-10, key
 
 
 def test_tableau_rejects(spx):
