@@ -16,7 +16,7 @@ GLPKDRV   := solver_glpk
 
 all: $(LIB) $(CLI) $(GLPKDRV) oracle
 
-$(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_tableau.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
+$(BUILD)/spx_kernels.o: $(SRC)/spx_kernels.hip $(SRC)/spx_kernels.h $(SRC)/spx_tableau.h $(SRC)/spx_tabdev.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -24,7 +24,7 @@ $(BUILD)/spx_reinv.o: $(SRC)/spx_reinv.hip $(SRC)/spx_reinv.h $(SRC)/spx_device.
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/spx_tableau.o: $(SRC)/spx_tableau.hip $(SRC)/spx_tableau.h $(SRC)/spx_grid.h $(SRC)/spx_loop.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
+$(BUILD)/spx_tableau.o: $(SRC)/spx_tableau.hip $(SRC)/spx_tableau.h $(SRC)/spx_tabdev.h $(SRC)/spx_grid.h $(SRC)/spx_loop.h $(SRC)/spx_device.h $(SRC)/spx_fold.h $(SRC)/spx_common.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -397,6 +397,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     uc.rows = rows;
     const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
     uc.grid = (int)std::max<int64_t>(1, (P.mloc + rows_per_wg - 1) / rows_per_wg);
+    if (P.tab) {  // k_tab_update: one lane per row, 256 rows per workgroup
+        uc.block = 256;
+        uc.rows = 1;
+        uc.grid = (int)std::max<int64_t>(1, (P.mloc + 255) / 256);
+    }
 
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
@@ -420,8 +425,15 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // window tableau: the persistent tableau loop (k_tab_loop) unless told not to
     if (P.tab && G == 1 && P.ratio != RATIO_HARRIS &&
         !(x->opts.flags & (SPX_FLAG_STAMPS | SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
-        HIP_TRY(tab_loop_prepare(P, x->cus, x->lcfg));
+        HIP_TRY(tab_loop_prepare(P, x->cus, x->opts.price_grid, x->lcfg));
         if (x->lcfg.ok) {
+            size_t xpb = 0, xub = 0;
+            tab_loop_partial_bytes(x->lcfg, &xpb, &xub);
+            unsigned char *xp = nullptr, *xu = nullptr;
+            SPX_TRY(x->alloc(&xp, xpb));
+            SPX_TRY(x->alloc(&xu, xub));
+            x->la.xp = xp;
+            x->la.xu = xu;
             SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
             SPX_TRY(x->alloc(&x->la.up, (size_t)x->lcfg.grid));
             SPX_TRY(x->alloc(&x->la.ls, 1));

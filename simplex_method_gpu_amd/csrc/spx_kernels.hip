@@ -32,6 +32,7 @@
 #include "spx_fold.h"
 #include "spx_kernels.h"
 #include "spx_tableau.h"
+#include "spx_tabdev.h"
 
 namespace spx {
 
@@ -251,47 +252,42 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (argmin_better(key, j, best, bj)) { best = key; bj = j; bw = wn; be = e; }
     };
     if constexpr (WM == 3) {
-        // window tableau: TPC columns per wave in flight; lane s < tau holds
-        // Wt[j][s]; r_tau.A_j = T_w[q,j] + sum_s U[q][s] Wt[j][s] and
-        // e_j = dw[j] + sum_s SY[s] Wt[j][s] + SY[tau] r_tau.A_j
-        constexpr int TPC = 4;
-        const int64_t qq = pend ? st->q : 0;
-        for (int idx = idx0; idx < nlist; idx += stride * TPC) {
-            int64_t jj[TPC];
-            double wv[TPC], tq[TPC], dv[TPC], sa[TPC], wn[TPC];
-#pragma unroll
-            for (int c = 0; c < TPC; ++c) {
-                const int ic = idx + c * stride;
-                jj[c] = ic < nlist ? (int64_t)P.nb_list[ic] : -1;
-            }
-#pragma unroll
-            for (int c = 0; c < TPC; ++c) {
-                const int64_t j = jj[c] < 0 ? 0 : jj[c];
-                wv[c] = (pend && lane < tau) ? P.Wt[j * KW + lane] : 0.0;
-                tq[c] = pend ? P.T[j * L + qq] : 0.0;
-                dv[c] = P.dw[j];
-                sa[c] = syl * wv[c];
-                wn[c] = uq * wv[c];
-            }
-            if (pend) {
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-                    for (int c = 0; c < TPC; ++c) {
-                        const double ta = __shfl_xor(sa[c], off, 64);
-                        const double tb = __shfl_xor(wn[c], off, 64);
-                        sa[c] += ta;
-                        wn[c] += tb;
-                    }
-            }
-#pragma unroll
-            for (int c = 0; c < TPC; ++c) {
-                if (jj[c] < 0) continue;
-                const double w = tq[c] + wn[c];
-                if (pend && lane == 0) P.Wt[jj[c] * KW + tau] = w;
-                consider(jj[c], pend ? fma(syp, w, dv[c] + sa[c]) : dv[c], w);
-            }
+        // window tableau (spx_tabdev.h): one lane per non-basic column, the
+        // window sums in pivot order inside the lane; a wave takes 64
+        // consecutive list slots
+        __shared__ double s_sy[64], s_uq[64];
+        if (tid < 64) {
+            s_sy[tid] = (pend && tid <= tau) ? P.SY[tid] : 0.0;
+            s_uq[tid] = (pend && tid < tau) ? P.U[st->q * KW + tid] : 0.0;
         }
+        __syncthreads();
+        const int64_t qq = pend ? st->q : 0;
+        for (int base = (blockIdx.x * WAVES + wave) * 64; base < nlist; base += stride * 64) {
+            const int idx = base + lane;
+            const bool cv = idx < nlist;
+            const int64_t j = cv ? (int64_t)P.nb_list[idx] : 0;
+            const double tq = (pend && cv) ? P.T[j * L + qq] : 0.0;
+            const double dv = cv ? P.dw[j] : 0.0;
+            double w, e;
+            tab_price_column(tq, dv, cv ? tau : -1, s_sy, s_uq, [&](int s2) { return P.Wt[j * KW + s2]; }, w, e);
+            if (!cv) continue;
+            if (pend) P.Wt[j * KW + tau] = w;
+            double key = e;
+            if (P.devex) {  // include/simplex.h SPX_PRICING_DEVEX
+                double wt = P.W[j];
+                if (pend) {
+                    if (j == dvx_leave) wt = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
+                    else {
+                        const double g = w / dvx_aq;
+                        wt = fmax(wt, g * g * dvx_wp);
+                    }
+                    P.W[j] = wt;
+                }
+                key = (e < -P.eps) ? -(e * e) / wt : INFINITY;
+            }
+            if (argmin_better(key, j, best, bj)) { best = key; bj = j; bw = w; be = e; }
+        }
+        wave_price_min(best, bj, bw, be);
     } else {
     // The first CH chunks of every column are loaded before the previous
     // column's reduction (and, for the first column, before the LDS fill), so
@@ -698,7 +694,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
-    const bool pf_ok = WIN && !RS && !P.tab && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
     if (pf_ok) {
         const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + pf_row * (P.L >> 1);
 #pragma unroll
@@ -841,18 +837,13 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
         // A_p staged in LDS once per workgroup (SPX_WIN_APLDS) instead of
         // every wave re-reading it through L1/L2 beside the B stream
-        const bool aplds = SPX_WIN_APLDS && L * 8 <= 65536 && !P.tab;
+        const bool aplds = SPX_WIN_APLDS && L * 8 <= 65536;
         if (SPX_WIN_APLDS && aplds) {
             dbl2* d = reinterpret_cast<dbl2*>(smem + Lds::bytes);
             for (int64_t kk = tid; kk < L2; kk += BLOCK) d[kk] = ap[kk];
             __syncthreads();
         }
-        if (P.tab) {
-            // window tableau: B_w[i,:] . A_p is the stored T_w[i, p]
-#pragma unroll
-            for (int u = 0; u < R; ++u)
-                if (u < nvalid && lane == 0) acc[u] = P.T[p * L + gr0 + u];
-        } else if (nvalid == R) {
+        if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
             static_assert(U == PFU, "prefetch and stream chunking agree");
@@ -1016,6 +1007,140 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     else
         update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
     stamp_tail(slot, t_tail, win);
+}
+
+// Window tableau FTRAN (spx_tabdev.h): one lane per row,
+// alpha_i = T_w[i,p] + sum_s U[i][s] Wt[p][s] — no B_w stream — then the
+// pending eta column into U, the basic columns' Wt entries, x_b, the ratio
+// test (v4:199-208) and, in the last workgroup, k_update's tail.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
+    DevState* st = P.st;
+    if (stopped(st)) return;
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ double s_wp[64];
+    // entering column, as k_update
+    double min_e = INFINITY, e_enter = 0.0;
+    int64_t p = INT64_MAX;
+    if (P.defer_price) {
+        PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
+        for (int g = tid; g < P.price_grid; g += BLOCK) {
+            const PricePartial v = P.price_partials[g];
+            if (argmin_better(v.val, v.idx, w.val, w.idx)) w = v;
+        }
+        wave_price_min(w.val, w.idx, w.w, w.pad);
+        __shared__ PricePartial s_pw[WAVES];
+        if (lane == 0) s_pw[wave] = w;
+        __syncthreads();
+        PricePartial t = s_pw[0];
+        for (int i = 1; i < WAVES; ++i)
+            if (argmin_better(s_pw[i].val, s_pw[i].idx, t.val, t.idx)) t = s_pw[i];
+        min_e = t.val;
+        p = t.idx;
+        e_enter = t.pad;
+    } else {
+        for (int g = 0; g < P.nin; ++g) {
+            const ArgMinEntry e = P.price_in[g * P.pr_stride];
+            if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; }
+        }
+    }
+    if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
+        if (blockIdx.x == 0 && tid == 0) {
+            st->p = p;
+            st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
+            st->status = ST_OPTIMAL;
+        }
+        return;
+    }
+    const int64_t it = st->iter;
+    const int par = (int)(it & 1);
+    const int64_t m = P.m, L = P.L;
+    const int KW = P.win;
+    const double* a_prev = par ? P.alpha1 : P.alpha0;
+    double* a_new = par ? P.alpha0 : P.alpha1;
+    const int nw = st->nw;
+    const int tau = nw - 1;
+    const bool pend = nw > 0;
+    const int64_t qp = st->q;
+    const double aqp = st->aq;
+    const bool upd_x = st->xb_applied < it;
+    if (tid < 64) s_wp[tid] = (tid < nw) ? P.Wt[p * KW + tid] : 0.0;
+    // s_x = r_tau . b = xw[q] + sum_{s<tau} U[q][s] Wt[n][s] (v4:347), as k_update
+    double sxw = 0.0;
+    if (pend) {
+        sxw = lane < tau ? P.U[qp * KW + lane] * P.Wt[P.n * KW + lane] : 0.0;
+        sxw = P.xw[qp] + wave_sum(sxw);
+        if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
+    }
+    const double s_x = upd_x ? sxw : 0.0;
+    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
+    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st, p);
+    if (P.defer_price) {
+        tpre.has_e = true;
+        tpre.e_enter = e_enter;
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + tid;
+    const bool rv = i < m;
+    UpdPartial wp = upd_empty();
+    if (rv) {
+        const double t = P.T[p * L + i];
+        const double ei = pend ? eta_entry(a_prev[i], i, qp, aqp) : 0.0;
+        const double a = tab_ftran_row(t, tau, ei, s_wp, [&](int s2) { return P.U[i * KW + s2]; });
+        const int64_t bix = P.b_ixs[i];
+        const double cb = P.c_B[i];
+        double x = P.x_b[i];
+        if (pend) {
+            P.U[i * KW + tau] = ei;
+            P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;  // r_tau.A_j of the basic columns
+        }
+        if (upd_x) {
+            x = fma(s_x, ei, x);
+            P.x_b[i] = x;
+        }
+        a_new[i] = a;
+        // one row: the candidate whatever its key (first index on ties, as
+        // k_update's argmin_better against the empty partial)
+        wp.theta = ratio_key(P, x, a);
+        wp.idx = i;
+        wp.nonpos = !(a > P.piv_tol);
+        wp.T = cb * a;
+        wp.a_w = a;
+        wp.cb_w = cb;
+        wp.bix_w = bix;
+    }
+    wp = wave_upd_merge(wp);
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
+    int* s_last = reinterpret_cast<int*>(smem + UpdLds<BLOCK>::last);
+    if (lane == 0) red[wave] = wp;
+    __syncthreads();
+    if (tid == 0) {
+        UpdPartial w = red[0];
+        for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
+        if (P.split_tail) {
+            P.upd_partials[blockIdx.x] = w;
+        } else {
+            UpdPartial* dstp = &P.upd_partials[blockIdx.x];
+            st_agent(&dstp->theta, w.theta);
+            st_agent(&dstp->idx, w.idx);
+            st_agent(&dstp->nonpos, w.nonpos);
+            st_agent(&dstp->T, w.T);
+            st_agent(&dstp->a_w, w.a_w);
+            st_agent(&dstp->cb_w, w.cb_w);
+            st_agent(&dstp->bix_w, w.bix_w);
+            drain_vmem();
+            const uint32_t tk = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            *s_last = (tk == gridDim.x - 1);
+        }
+    }
+    if (P.split_tail) return;  // k_tail merges after the kernel boundary
+    __syncthreads();
+    if (!*s_last) return;
+    update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
 }
 
 // Row-sharded tail (last workgroup of k_update on this rank): the local
@@ -1544,6 +1669,14 @@ static hipError_t launch_update_b(const Params& P, const UpdateCfg& c, hipStream
 }
 
 hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (P.tab) {  // window tableau: k_tab_update, 256 rows per workgroup
+        const size_t lds = UpdLds<256>::bytes;
+        if (e0 || e1)
+            hipExtLaunchKernelGGL((k_tab_update<256>), dim3(c.grid), dim3(256), (uint32_t)lds, s, e0, e1, 0, P);
+        else
+            hipLaunchKernelGGL((k_tab_update<256>), dim3(c.grid), dim3(256), lds, s, P);
+        return hipGetLastError();
+    }
     switch (c.block) {
         case 256: return launch_update_b<256>(P, c, s, e0, e1);
         case 512: return launch_update_b<512>(P, c, s, e0, e1);

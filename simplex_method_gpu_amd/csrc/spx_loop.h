@@ -42,6 +42,8 @@ struct LoopArgs {
     unsigned long long* clock;  // optional: per pass {start, barrier 1, barrier 2} (s_memrealtime), WG 0
     int32_t npasses;            // passes to run (the window must not fill)
     int32_t pad;
+    void* xp;                   // tableau loop: G pricing partials with the candidate's window row
+    void* xu;                   // tableau loop: G ratio-test partials with the candidate's eta row
 };
 
 struct LoopCfg {
@@ -50,6 +52,8 @@ struct LoopCfg {
     bool lds_r = true;  // pending base row in LDS next to y_w
     size_t lds_bytes = 0;
     bool ok = false;    // the persistent path is usable for this context
+    int cpw = 0;        // tableau loop: list slots cached per wave
+    int rw = 0;         // tableau loop: rows per wave
 };
 
 // Shapes the launch for P (window mode, one rank); ok = false when the device

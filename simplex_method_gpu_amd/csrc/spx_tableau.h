@@ -15,8 +15,11 @@ hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s);
 // T_w = B_w A (B_w = P.B0, row-major): after a reinversion or a warm start.
 hipError_t launch_tab_build(const Params& P, hipStream_t s);
 // Persistent tableau loop (k_tab_loop): whole passes in one cooperative
-// launch, one workgroup per CU; ok = false when it cannot be used.
-hipError_t tab_loop_prepare(const Params& P, int cus, LoopCfg& c);
+// launch; grid_hint > 0 forces the workgroup count; ok = false when it cannot
+// be used (caches do not fit, or no cooperative launch).
+hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c);
 hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s);
+// bytes of the loop's partial buffers (LoopArgs::xp, ::xu) for c.grid workgroups
+void tab_loop_partial_bytes(const LoopCfg& c, size_t* xp, size_t* xu);
 
 }  // namespace spx
