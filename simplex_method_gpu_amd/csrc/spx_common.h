@@ -63,6 +63,10 @@ __device__ __forceinline__ T ld_agent(const T* p) {
     return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Workgroup barrier for data exchanged through LDS only: the LDS operations
+// complete (lgkmcnt), global loads and stores stay in flight across it
+// (__syncthreads()'s workgroup fence would wait for them: vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ bool stopped(const DevState* st) {
     return st->status != ST_RUNNING || st->iter >= st->limit;

@@ -11,7 +11,8 @@
 //   T_w += U Wt^T   (m x n x nf, U = the eta columns, Wt[j][tau] = r_tau.A_j)
 //   dw  += SY Wt^T
 // which moves 16 L n bytes per window instead of 8(m+1)(n-m) + 8m^2 per pivot.
-// k_tab_build rebuilds T_w = B_w A after a reinversion or a warm start.
+// k_tab_build rebuilds T_w = B_w A after a reinversion or a warm start;
+// k_tab_loop runs whole passes in one cooperative launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,20 +28,31 @@ namespace spx {
 
 namespace {
 
-// Workgroup = 4 waves; wave w owns TJ x 16 columns of T_w (its Wt fragments,
-// the MFMA A operand, lane: Wt[j0 + cl][4 s + kr], stay in registers) and
-// walks its row range 16 rows at a time: the U fragment (B operand, lane:
-// U[i + cl][4 s + kr], an L2 hit: U is m x KW) and the TJ accumulator tiles
-// of T_w (lane: T_w[i + cl, j0 + 16 jt + kr + 4 r]) of the next row block are
-// loaded before this block's ceil(nf/4) x TJ v_mfma_f64_16x16x4f64.  T_w is
-// read and written once per fold.
-template <int KW, int TJ>
+// ---------------------------------------------------------------------------
+// T_w += U Wt^T, dw += SY Wt^T.  A workgroup (4 waves) owns 64 columns of T_w
+// and a range of rows, walked 64 rows at a time.  Wave w keeps the Wt
+// fragments of its 16 columns in registers (MFMA A operand, lane:
+// Wt[j0 + cl][4 s + kr]).  The eta rows U[i0 .. i0+64) of a block — 32 KiB,
+// contiguous — are staged once per workgroup into LDS with 16-byte loads
+// (double-buffered: the next block's are loaded before this block's MFMAs)
+// and read from there as the B operand (lane: U[i + cl][4 s + kr]).  The 4
+// accumulator tiles of a wave (lane: T_w[i + 16 it + cl, j0 + kr + 4 r]) are
+// T_w itself, read and written once; the next block's tiles are also in
+// flight during this block's 4 x ceil(nf/4) v_mfma_f64_16x16x4f64.
+// ---------------------------------------------------------------------------
+constexpr int TF_RB = 64;  // rows per block
+constexpr int TF_UP = 68;  // LDS pitch of a staged eta row (doubles): 16-B aligned, spreads banks
+
+template <int KW>
 __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
     const DevState* st = P.st;
     const int nw = st->nw;
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
     constexpr int KS = KW / 4;
+    constexpr int KW2 = KW / 2;             // dbl2 per eta row
+    constexpr int UPT = TF_RB * KW2 / 256;  // dbl2 staged per thread per block
+    __shared__ __attribute__((aligned(16))) double Ub[2][TF_RB * TF_UP];
     const int ks = (nf + 3) / 4;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -49,80 +61,95 @@ __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
     const double* __restrict__ U = P.U;
     const double* __restrict__ Wt = P.Wt;
     double* __restrict__ T = P.T;
-    const int64_t cb = (int64_t)blockIdx.y * (4 * 16 * TJ);  // this workgroup's columns
+    const int64_t cb = (int64_t)blockIdx.y * 64;  // this workgroup's columns
 
-    if (blockIdx.x == 0) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t], fixed t order
-        for (int64_t j = cb + tid; j < cb + 4 * 16 * TJ && j < n; j += 256) {
-            double d = 0.0;
-            for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
-            P.dw[j] += d;
-        }
+    if (blockIdx.x == 0 && tid < 64 && cb + tid < n) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t]
+        const int64_t j = cb + tid;
+        double d = 0.0;
+        for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
+        P.dw[j] += d;
     }
-    const int64_t j0 = cb + (int64_t)wave * 16 * TJ;
-    const int64_t per = ((m + gridDim.x - 1) / gridDim.x + 15) / 16 * 16;
+    const int64_t per = ((m + gridDim.x - 1) / gridDim.x + TF_RB - 1) / TF_RB * TF_RB;
     const int64_t i_lo = (int64_t)blockIdx.x * per;
     const int64_t i_hi = (i_lo + per < m) ? i_lo + per : m;
-    if (j0 >= n || i_lo >= i_hi) return;
+    if (cb >= n || i_lo >= i_hi) return;  // uniform per workgroup
+    const int64_t j0 = cb + 16 * wave;
 
-    double wf[TJ][KS];
+    double wf[KS];
 #pragma unroll
-    for (int jt = 0; jt < TJ; ++jt) {
-        const int64_t j = j0 + 16 * jt + cl;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int t = 4 * s + kr;
-            wf[jt][s] = (j < n && t < nf) ? Wt[j * KW + t] : 0.0;
-        }
+    for (int s = 0; s < KS; ++s) {
+        const int t = 4 * s + kr;
+        wf[s] = (j0 + cl < n && t < nf) ? Wt[(j0 + cl) * KW + t] : 0.0;
     }
-    bool cok[TJ][4];
+    bool jok[4];
 #pragma unroll
-    for (int jt = 0; jt < TJ; ++jt)
+    for (int r = 0; r < 4; ++r) jok[r] = j0 + kr + 4 * r < n;
+
+    auto stage_load = [&](int64_t i0, dbl2 (&ur)[UPT]) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cok[jt][r] = j0 + 16 * jt + kr + 4 * r < n;
-    auto load = [&](int64_t i0, double (&uf)[KS], dbl4 (&acc)[TJ]) {
-        const int64_t i = i0 + cl;
-        const bool iok = i < i_hi;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int t = 4 * s + kr;
-            uf[s] = (iok && t < nf) ? U[i * KW + t] : 0.0;
+        for (int k = 0; k < UPT; ++k) {
+            const int pce = tid + 256 * k;
+            const int64_t i = i0 + pce / KW2;
+            ur[k] = (i < i_hi) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
         }
+    };
+    auto stage_write = [&](int buf, const dbl2 (&ur)[UPT]) {
 #pragma unroll
-        for (int jt = 0; jt < TJ; ++jt)
+        for (int k = 0; k < UPT; ++k) {
+            const int pce = tid + 256 * k;
+            *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * TF_UP + 2 * (pce % KW2)]) = ur[k];
+        }
+    };
+    auto tile_load = [&](int64_t i0, dbl4 (&acc)[4]) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int64_t i = i0 + 16 * it + cl;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                acc[jt][r] = (iok && cok[jt][r]) ? T[(j0 + 16 * jt + kr + 4 * r) * L + i] : 0.0;
+                acc[it][r] = (jok[r] && i < i_hi) ? T[(j0 + kr + 4 * r) * L + i] : 0.0;
+        }
     };
-    double uf[KS];
-    dbl4 acc[TJ];
-    load(i_lo, uf, acc);
-    for (int64_t i0 = i_lo; i0 < i_hi; i0 += 16) {
-        double un[KS];
-        dbl4 an[TJ];
-        const bool more = i0 + 16 < i_hi;
-        if (more) load(i0 + 16, un, an);
+
+    dbl2 ur[UPT];
+    dbl4 acc[4];
+    stage_load(i_lo, ur);
+    tile_load(i_lo, acc);
+    stage_write(0, ur);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t i0 = i_lo; i0 < i_hi; i0 += TF_RB, buf ^= 1) {
+        const bool more = i0 + TF_RB < i_hi;
+        dbl4 nxt[4];
+        if (more) {
+            stage_load(i0 + TF_RB, ur);
+            tile_load(i0 + TF_RB, nxt);
+        }
+        const double* ub = Ub[buf];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             if (s < ks) {
 #pragma unroll
-                for (int jt = 0; jt < TJ; ++jt)
-                    acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(wf[jt][s], uf[s], acc[jt], 0, 0, 0);
+                for (int it = 0; it < 4; ++it) {
+                    const double bv = ub[(16 * it + cl) * TF_UP + 4 * s + kr];
+                    acc[it] = __builtin_amdgcn_mfma_f64_16x16x4f64(wf[s], bv, acc[it], 0, 0, 0);
+                }
             }
         }
-        const int64_t i = i0 + cl;
-        if (i < i_hi) {
 #pragma unroll
-            for (int jt = 0; jt < TJ; ++jt)
+        for (int it = 0; it < 4; ++it) {
+            const int64_t i = i0 + 16 * it + cl;
+            if (i < i_hi) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (cok[jt][r]) T[(j0 + 16 * jt + kr + 4 * r) * L + i] = acc[jt][r];
+                    if (jok[r]) T[(j0 + kr + 4 * r) * L + i] = acc[it][r];
+            }
         }
         if (more) {
+            stage_write(buf ^ 1, ur);
 #pragma unroll
-            for (int s = 0; s < KS; ++s) uf[s] = un[s];
-#pragma unroll
-            for (int jt = 0; jt < TJ; ++jt) acc[jt] = an[jt];
+            for (int it = 0; it < 4; ++it) acc[it] = nxt[it];
         }
+        __syncthreads();
     }
 }
 
@@ -199,19 +226,17 @@ __global__ __launch_bounds__(256) void k_tab_build(Params P) {
 //   rows: wave w owns rows row0 + w + r W, one per lane r; registers hold
 //     alpha_prev, b_ixs, c_B, x_b, LDS the row's eta coefficients U[i][.].
 // Per pass (the arithmetic of k_price WM 3 / k_tab_update, spx_tabdev.h):
-//   A  lane c prices column c: T_w[q, j] (one gather per wave, with the
-//      re-cache of list slots the last pivot changed) and the window sums
-//      from LDS; workgroup argmin -> partial WITH the candidate's window
-//      row.                                                    -> barrier 1
-//   B  every workgroup loads all pricing partials and rows in one round
-//      trip (same p everywhere, Wt[p][.] with it); lane r: alpha_i from
-//      T_w[i,p] and its LDS row; x_b; ratio test -> partial WITH the
-//      candidate's eta row U[i][.].                            -> barrier 2
-//   C  every workgroup loads all ratio partials and rows in one round trip
-//      (q, s_y, and U[q][.] for the next pricing); workgroup 0 writes the
-//      bookkeeping; owners note the two list slots the pivot changed; the
-//      new pending base row B_w[q,:] goes to Qrows for k_fold, one slice
-//      per workgroup.
+//   A  lane c prices column c: T_w[q, j] (one gather per wave, issued with
+//      the re-cache of list slots the last pivot changed) and the window
+//      sums from LDS; workgroup argmin -> partial (with the candidate's
+//      window entry and list slot).                           -> barrier 1
+//   B  the column results of A go to HBM (off barrier 1's drain); every
+//      workgroup reduces the pricing partials (same p everywhere); lane r:
+//      alpha_i from T_w[i,p] and its LDS row; x_b; ratio test.  -> barrier 2
+//   C  every workgroup reduces the ratio-test partials (q, s_y) and loads
+//      U[q][.] for the next pricing; workgroup 0 writes the bookkeeping;
+//      owners note the two list slots the pivot changed; the new pending
+//      base row B_w[q,:] goes to Qrows for k_fold, one slice per workgroup.
 // Global copies of everything cached (Wt, U, W, x_b, alpha) are written as
 // they change, so the two-kernel passes, the folds and readbacks see the
 // same state.
@@ -222,26 +247,20 @@ constexpr int TKP = TKW + 1;  // LDS row pitch (doubles): lane-per-row reads hit
 #define SPX_TAB_CLK 0  // diagnostic stamp placement: 0 = phases A / B / C
 #endif
 
-struct alignas(16) TabPP {  // pricing partial + the candidate's window row
+struct alignas(16) TabPP {  // pricing partial: candidate, its window entry, its list slot
     double val;
     int64_t idx;
     double w;
     double e;
     int64_t slot;
     int64_t pad;
-    double row[TKW];
-};
-struct alignas(16) TabUP {  // ratio-test partial + the candidate's eta row
-    UpdPartial h;
-    double row[TKW];
 };
 
-struct TabPick {  // merged pricing candidate and the partial it came from
+struct TabPick {  // a pricing candidate being merged
     double val;
     int64_t idx;
     double w, e;
     int64_t slot;
-    int32_t g;
 };
 __device__ __forceinline__ void pick_merge(TabPick& a, const TabPick& b) {
     if (argmin_better(b.val, b.idx, a.val, a.idx)) a = b;
@@ -253,10 +272,10 @@ __device__ __forceinline__ TabPick pick_shfl_xor(const TabPick& v, int off) {
     o.w = __shfl_xor(v.w, off, 64);
     o.e = __shfl_xor(v.e, off, 64);
     o.slot = __shfl_xor(v.slot, off, 64);
-    o.g = __shfl_xor(v.g, off, 64);
     return o;
 }
-// ratio-test merge carrying the source partial (UpdPartial::pad) with the winner
+
+// ratio-test merge carrying UpdPartial::pad (the winner's eta entry) with the winner
 __device__ __forceinline__ void tup_merge(UpdPartial& a, const UpdPartial& b) {
     const bool take = argmin_better(b.theta, b.idx, a.theta, a.idx);
     upd_merge(a, b);
@@ -302,8 +321,7 @@ struct TabCache {
     }
 };
 
-// TPR: partial-row doubles per loading thread (64 / (BLOCK / G) at most)
-template <int BLOCK, int TPR>
+template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int cpw, int rw) {
     constexpr int WAVES = BLOCK / 64;
     __shared__ TabLds<WAVES> S;
@@ -311,7 +329,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TabCache<WAVES> C(smem, cpw);
     TabPP* const XP = reinterpret_cast<TabPP*>(La.xp);
-    TabUP* const XU = reinterpret_cast<TabUP*>(La.xu);
+    UpdPartial* const XU = reinterpret_cast<UpdPartial*>(La.xu);
     DevState* st = P.st;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -328,6 +346,8 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     if (nw >= KW) return;  // the host folds first
     int64_t q = st->q;
     double aq = st->aq;
+    int64_t q_prev = -1;   // the pivot before the pending one (this launch only)
+    double aq_prev = 0.0;
     int64_t xb_applied = st->xb_applied;
     const int cnt = st->nb_count;
     int64_t lastv = P.nb_list[cnt - 1];  // the list's last slot (it receives every leaving column)
@@ -346,11 +366,6 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     const int lr = wave * rw + rs;
     const int64_t irow = row0 + wave + (int64_t)rs * WAVES;
     const bool rv = lane < rw && irow < row1;
-    // partial loading: tpp threads per partial, each a slice of its row
-    const int tpp = BLOCK / G;
-    const int pg = tid / tpp, psub = tid - pg * tpp;
-    const bool pok = pg < G;
-    const int per = (TKW + tpp - 1) / tpp;
     // this workgroup's slice of a base row (Qrows staging for k_fold)
     const int64_t qsl = ((L + G - 1) / G + 1) / 2 * 2;
     const int64_t qk0 = (int64_t)blockIdx.x * qsl;
@@ -361,17 +376,14 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         S.SY[tid] = (tid < nw) ? P.SY[tid] : 0.0;
         S.Uq[tid] = (nw > 0 && tid < nw - 1) ? P.U[q * KW + tid] : 0.0;
     }
-    if (nw > 0) {  // the pending pivot's base row (B_w changed at the last fold)
-        for (int64_t k = qk0 + tid; k < qk1; k += BLOCK) P.Qrows[(int64_t)(nw - 1) * L + k] = P.B0[q * L + k];
-        if (wg0 && tid < nw - 1) P.Urows[(int64_t)(nw - 1) * KW + tid] = P.U[q * KW + tid];
-    }
+    if (nw > 0 && wg0 && tid < nw - 1) P.Urows[(int64_t)(nw - 1) * KW + tid] = P.U[q * KW + tid];
     if (cv) {
         const int32_t j = P.nb_list[vid + lane * stride];
         C.col[ls] = j;
         C.dwc[ls] = P.dw[j];
         C.wc[ls] = P.devex ? P.W[j] : 1.0;
     }
-    __syncthreads();
+    lds_barrier();
     for (int c = 0; c < cpw; ++c) {  // window rows: one coalesced row per step
         if (vid + c * stride >= cnt) break;
         const int64_t j = C.col[wave * cpw + c];
@@ -390,12 +402,61 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         if (i >= row1) break;
         C.ur[(int64_t)(wave * rw + r) * TKP + lane] = (lane < nw - 1) ? P.U[i * KW + lane] : 0.0;
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t target = 0;
     // list slots the last pivot changed, owned by this wave: re-cached at the
     // start of the next pricing phase (their window rows then are visible)
     int rc_ls0 = -1, rc_ls1 = -1;
     int64_t rc_j0 = 0, rc_j1 = 0;
+    double rc_basic = 0.0;  // the leaving column's window entry for the pivot that made it leave
+    // results of a pass that go to HBM one phase later (after the next
+    // barrier 1, so no barrier's drain waits for them): this lane's row
+    // (eta entry, its basic column's window entry, x_b, alpha) and, in
+    // workgroup 0, the pivot's bookkeeping (v4:339-342)
+    bool rp = false, rp_pend = false;
+    int r_tau = 0;
+    int64_t r_it = 0, r_bx = -1;
+    double r_ei = 0.0, r_bv = 0.0;
+    bool bk = false;
+    int64_t bk_kp = 0, bk_lastv = 0, bk_p = 0, bk_leave = 0, bk_qn = 0, bk_it = 0;
+    int bk_nw = 0;
+    double bk_cp = 0.0, bk_sy = 0.0, bk_aq = 0.0, bk_mine = 0.0, bk_wp = 0.0;
+    auto flush = [&]() {
+        if (rp && rv) {
+            if (rp_pend) {
+                st_agent(&P.U[irow * KW + r_tau], r_ei);
+                st_agent(&P.Wt[r_bx * KW + r_tau], r_bv);
+            }
+            P.x_b[irow] = xbr;
+            ((r_it & 1) ? P.alpha0 : P.alpha1)[irow] = apr;
+        }
+        rp = false;
+        if (bk && wg0 && tid == 0) {
+            if (bk_kp != cnt - 1) {
+                st_agent(&P.nb_list[bk_kp], (int32_t)bk_lastv);
+                st_agent(&P.nb_pos[bk_lastv], (int32_t)bk_kp);
+            }
+            st_agent(&P.nb_pos[bk_p], (int32_t)-1);
+            st_agent(&P.nb_list[cnt - 1], (int32_t)bk_leave);
+            st_agent(&P.nb_pos[bk_leave], (int32_t)(cnt - 1));
+            st_agent(&P.c_B[bk_qn], bk_cp);
+            st_agent(&P.b_ixs[bk_qn], bk_p);
+            P.SY[bk_nw] = bk_sy;
+            st->aq = bk_aq;
+            st->s_y = bk_sy;
+            st->nw = bk_nw + 1;
+            st->xb_applied = bk_it;
+            st->p = bk_p;
+            st->q = bk_qn;
+            st->min_e = bk_mine;
+            st->iter = bk_it + 1;
+            if (P.devex) {
+                st->leave = bk_leave;
+                st->wp = bk_wp;
+            }
+        }
+        bk = false;
+    };
 
     for (int pass = 0; pass < La.npasses && it < limit; ++pass) {
         const bool pend = nw > 0;
@@ -404,15 +465,16 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         if (clk) clk[0] = rtime();
 
         // ================= phase A: pricing, lane c <-> column slot c
-        // (issued together: the re-cache loads, T_w[q, j] of every column,
-        // and the x_b update's s_x = r_tau . b for phase B)
         if (rc_ls0 >= 0 || rc_ls1 >= 0) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int lsn = h ? rc_ls1 : rc_ls0;
                 if (lsn < 0) continue;
                 const int64_t jn = h ? rc_j1 : rc_j0;
-                C.wt[(int64_t)lsn * TKP + lane] = (lane < tau) ? ld_agent(&P.Wt[jn * KW + lane]) : 0.0;
+                // the leaving column's entry for the last pivot: its basic-column
+                // value (stored one phase later, so not yet visible)
+                C.wt[(int64_t)lsn * TKP + lane] =
+                    (h && lane == tau - 1) ? rc_basic : ((lane < tau) ? ld_agent(&P.Wt[jn * KW + lane]) : 0.0);
                 if (lane == 0) {
                     C.col[lsn] = (int32_t)jn;
                     C.dwc[lsn] = P.dw[jn];
@@ -421,105 +483,110 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             }
             rc_ls0 = rc_ls1 = -1;
         }
+        // s_x = r_tau . b for phase B's x_b update (k_tab_update's formula)
         double sxw = 0.0;
         if (pend) {
             sxw = lane < tau ? S.Uq[lane] * ld_agent(&P.Wt[n * KW + lane]) : 0.0;
             sxw = P.xw[q] + wave_sum(sxw);
-            if (wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
         }
-        TabPick best{INFINITY, INT64_MAX, 0.0, 0.0, -1, (int32_t)blockIdx.x};
+        TabPick best{INFINITY, INT64_MAX, 0.0, 0.0, -1};
+        const int64_t cj = cv ? (int64_t)C.col[ls] : 0;
+        double cw = 0.0, cwt = 0.0;  // this column's window entry and Devex weight, stored in phase B
         {
-            const int64_t j = cv ? (int64_t)C.col[ls] : 0;
-            const double tq = (pend && cv) ? P.T[j * L + q] : 0.0;
+            const double tq = (pend && cv) ? P.T[cj * L + q] : 0.0;
             const double dv = cv ? C.dwc[ls] : 0.0;
             const double* wrow = C.wt + (int64_t)ls * TKP;
-            double w, e;
-            tab_price_column(tq, dv, cv ? tau : -1, S.SY, S.Uq, [&](int s2) { return wrow[s2]; }, w, e);
+            double e;
+            tab_price_column(tq, dv, cv ? tau : -1, S.SY, S.Uq, [&](int s2) { return wrow[s2]; }, cw, e);
 #if SPX_TAB_CLK == 1  // diagnostic: {pass start, column done, barrier 1 done}
             if (clk) clk[1] = rtime();
 #endif
             if (cv) {
-                if (pend) {
-                    C.wt[(int64_t)ls * TKP + tau] = w;
-                    st_agent(&P.Wt[j * KW + tau], w);
-                }
+                if (pend) C.wt[(int64_t)ls * TKP + tau] = cw;
                 double key = e;
                 if (P.devex) {  // include/simplex.h SPX_PRICING_DEVEX, as k_price
-                    double wt = C.wc[ls];
+                    cwt = C.wc[ls];
                     if (pend) {
-                        if (j == dleave) wt = fmax(dwp / (aq * aq), 1.0);
+                        if (cj == dleave) cwt = fmax(dwp / (aq * aq), 1.0);
                         else {
-                            const double g = w / aq;
-                            wt = fmax(wt, g * g * dwp);
+                            const double g = cw / aq;
+                            cwt = fmax(cwt, g * g * dwp);
                         }
-                        C.wc[ls] = wt;
-                        st_agent(&P.W[j], wt);
+                        C.wc[ls] = cwt;
                     }
-                    key = (e < -P.eps) ? -(e * e) / wt : INFINITY;
+                    key = (e < -P.eps) ? -(e * e) / cwt : INFINITY;
                 }
-                best = TabPick{key, j, w, e, (int64_t)vid + (int64_t)lane * stride, (int32_t)(wave * 64 + lane)};
+                best.val = key;
+                best.idx = cj;
             }
+            // wave argmin on (key, column); the winner's entry, reduced cost
+            // and slot come from its lane
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) pick_merge(best, pick_shfl_xor(best, off));
+            for (int off = 32; off > 0; off >>= 1) {
+                const double k2 = __shfl_xor(best.val, off, 64);
+                const int64_t j2 = __shfl_xor(best.idx, off, 64);
+                if (argmin_better(k2, j2, best.val, best.idx)) {
+                    best.val = k2;
+                    best.idx = j2;
+                }
+            }
+            const unsigned long long wb = __ballot(cv && cj == best.idx);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            best.w = __shfl(cw, wl, 64);
+            best.e = __shfl(e, wl, 64);
+            best.slot = (int64_t)vid + (int64_t)wl * stride;
         }
         if (lane == 0) S.ppick[wave] = best;
-        __syncthreads();
-        {
+        lds_barrier();
+        if (tid == 0) {
             TabPick w = S.ppick[0];
             for (int i = 1; i < WAVES; ++i) pick_merge(w, S.ppick[i]);
-            // the winning lane's wave copies its window row into the partial
             TabPP* d = &XP[blockIdx.x];
-            if (w.idx != INT64_MAX && wave == (w.g >> 6)) {
-                const int wls = wave * cpw + (w.g & 63);
-                st_agent(&d->row[lane], C.wt[(int64_t)wls * TKP + lane]);
-            }
-            if (tid == 0) {
-                st_agent(&d->val, w.val);
-                st_agent(&d->idx, w.idx);
-                st_agent(&d->w, w.w);
-                st_agent(&d->e, w.e);
-                st_agent(&d->slot, w.slot);
-            }
+            st_agent(&d->val, w.val);
+            st_agent(&d->idx, w.idx);
+            st_agent(&d->w, w.w);
+            st_agent(&d->e, w.e);
+            st_agent(&d->slot, w.slot);
         }
         target += (uint32_t)G;
         if (!grid_sync(La.ls, target, &s_ok)) return;
-#if SPX_TAB_CLK != 2
+#if SPX_TAB_CLK == 0 || SPX_TAB_CLK == 1
         if (clk) clk[SPX_TAB_CLK == 1 ? 2 : 1] = rtime();
 #endif
 
-        // ================= phase B: entering column (all partials and rows
-        // in one round trip), FTRAN + ratio test
+        // ================= phase B: entering column, FTRAN + ratio test
+        // Deferred writes, drained at barrier 2: phase A's column results,
+        // the last pass's row results and bookkeeping, and the pending
+        // pivot's base row slice for k_fold.
+        if (cv && pend) {
+            st_agent(&P.Wt[cj * KW + tau], cw);
+            if (P.devex) st_agent(&P.W[cj], cwt);
+        }
+        if (pend && wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
+        flush();
+        if (pend)
+            for (int64_t k = qk0 + tid; k < qk1; k += BLOCK) P.Qrows[(int64_t)tau * L + k] = P.B0[q * L + k];
         {
-            TabPick w{INFINITY, INT64_MAX, 0.0, 0.0, -1, 0};
-            double rowv[TPR];
-            if (pok) {
-                const TabPP* d = &XP[pg];
-                if (psub == 0) w = TabPick{ld_agent(&d->val), ld_agent(&d->idx), ld_agent(&d->w), ld_agent(&d->e),
-                                           ld_agent(&d->slot), pg};
-#pragma unroll
-                for (int k = 0; k < TPR; ++k)
-                    if (k < per && psub * per + k < TKW) rowv[k] = ld_agent(&d->row[psub * per + k]);
+            TabPick w{INFINITY, INT64_MAX, 0.0, 0.0, -1};
+            for (int g = tid; g < G; g += BLOCK) {
+                const TabPP* d = &XP[g];
+                w = TabPick{ld_agent(&d->val), ld_agent(&d->idx), ld_agent(&d->w), ld_agent(&d->e),
+                            ld_agent(&d->slot)};
             }
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) pick_merge(w, pick_shfl_xor(w, off));
             if (lane == 0) S.ppick[wave] = w;
-            __syncthreads();
-            TabPick t = S.ppick[0];
-            for (int i = 1; i < WAVES; ++i) pick_merge(t, S.ppick[i]);
-            if (pok && pg == t.g && t.idx != INT64_MAX) {
-#pragma unroll
-                for (int k = 0; k < TPR; ++k)
-                    if (k < per && psub * per + k < TKW) S.Wp[psub * per + k] = rowv[k];
+            lds_barrier();
+            if (tid == 0) {
+                TabPick t = S.ppick[0];
+                for (int i = 1; i < WAVES; ++i) pick_merge(t, S.ppick[i]);
+                S.pwin = t;
             }
-            if (tid == 0) S.pwin = t;
-            __syncthreads();
+            lds_barrier();
         }
         const TabPick pw = S.pwin;
         const int64_t p = pw.idx;
         const double min_e = pw.val;
-#if SPX_TAB_CLK == 2  // diagnostic: {pass start, barrier 1 done, p and Wt[p] known}
-        if (clk) clk[1] = rtime();
-#endif
         if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
             if (wg0 && tid == 0) {
                 st->p = p;
@@ -528,92 +595,113 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             }
             break;
         }
-        // the winner's own window entry Wt[p][tau] (the row copy may predate it)
-        if (tid == 0 && pend) S.Wp[tau] = pw.w;
+        double rei = 0.0;  // this lane's row: eta entry of the pending pivot
         {
-            double* a_new = (it & 1) ? P.alpha0 : P.alpha1;
+            // the entering column's window row: entries s < tau from earlier
+            // passes, entry tau from its pricer's partial; a column that left
+            // at the last pivot has its entry tau-1 (its basic value) still in
+            // flight: (q == q_prev) ? aq_prev : 0
+            if (tid < KW) {
+                double v = 0.0;
+                if (tid == tau) v = pw.w;
+                else if (tid < tau)
+                    v = (p == lastv && tid == tau - 1 && q_prev >= 0) ? ((q == q_prev) ? aq_prev : 0.0)
+                                                                      : ld_agent(&P.Wt[p * KW + tid]);
+                S.Wp[tid] = v;
+            }
             const bool upd_x = xb_applied < it;
             const double tcol = rv ? P.T[p * L + irow] : 0.0;
             const double s_x = upd_x ? sxw : 0.0;
-            __syncthreads();
-            UpdPartial wp = upd_empty();
+            lds_barrier();
+#if SPX_TAB_CLK == 2  // diagnostic: {pass start, barrier 1 done, p and Wt[p] known}
+            if (clk) clk[1] = rtime();
+#endif
+            double th = INFINITY, tT = 0.0, a = 0.0;
+            int64_t ti = INT64_MAX;
             if (rv) {
-                const double ei = pend ? eta_entry(apr, irow, q, aq) : 0.0;
+                rei = pend ? eta_entry(apr, irow, q, aq) : 0.0;
                 const double* urow = C.ur + (int64_t)lr * TKP;
-                const double a = tab_ftran_row(tcol, tau, ei, S.Wp, [&](int s2) { return urow[s2]; });
-                if (pend) {
-                    C.ur[(int64_t)lr * TKP + tau] = ei;
-                    st_agent(&P.U[irow * KW + tau], ei);
-                    st_agent(&P.Wt[bxr * KW + tau], (irow == q) ? aq : 0.0);
-                }
-                if (upd_x) {
-                    xbr = fma(s_x, ei, xbr);
-                    P.x_b[irow] = xbr;
-                }
+                a = tab_ftran_row(tcol, tau, rei, S.Wp, [&](int s2) { return urow[s2]; });
+                if (pend) C.ur[(int64_t)lr * TKP + tau] = rei;
+                if (upd_x) xbr = fma(s_x, rei, xbr);
                 apr = a;
-                a_new[irow] = a;
-                wp.theta = ratio_key(P, xbr, a);
-                wp.idx = irow;
-                wp.nonpos = !(a > P.piv_tol);
-                wp.T = cbr * a;
-                wp.a_w = a;
-                wp.cb_w = cbr;
-                wp.bix_w = bxr;
-                wp.pad = wave * 64 + lane;
+                th = ratio_key(P, xbr, a);
+                ti = irow;
+                tT = cbr * a;
+                // for the deferred write
+                rp = true;
+                rp_pend = pend;
+                r_tau = tau;
+                r_it = it;
+                r_ei = rei;
+                r_bx = bxr;
+                r_bv = (irow == q) ? aq : 0.0;  // r_tau . A_j of the basic column j of this row
             }
+#if SPX_TAB_CLK == 3  // diagnostic: {pass start, FTRAN rows done, partial written}
+            if (clk) clk[1] = rtime();
+#endif
+            // wave merge: argmin on (theta, row) and the c_B.alpha sum
+            // together; alpha <= 0 counted by ballot; the winner's scalars
+            // (and its eta entry, U[q][tau] for the next pricing) from its lane
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const UpdPartial o = tup_shfl_xor(wp, off);
-                UpdPartial lo = (lane & off) ? o : wp;
-                const UpdPartial hi = (lane & off) ? wp : o;
-                tup_merge(lo, hi);
-                wp = lo;
+            for (int off = 32; off > 0; off >>= 1) {
+                const double t2 = __shfl_xor(th, off, 64);
+                const int64_t i2 = __shfl_xor(ti, off, 64);
+                tT += __shfl_xor(tT, off, 64);
+                if (argmin_better(t2, i2, th, ti)) {
+                    th = t2;
+                    ti = i2;
+                }
             }
+            UpdPartial wp = upd_empty();
+            wp.theta = th;
+            wp.idx = ti;
+            wp.T = tT;
+            wp.nonpos = __popcll(__ballot(rv && !(a > P.piv_tol)));
+            const unsigned long long wb = __ballot(rv && irow == ti);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            wp.a_w = __shfl(a, wl, 64);
+            wp.cb_w = __shfl(cbr, wl, 64);
+            wp.bix_w = __shfl(bxr, wl, 64);
+            wp.pad = __double_as_longlong(__shfl(rei, wl, 64));
             if (lane == 0) S.ured[wave] = wp;
-            __syncthreads();
-            UpdPartial w = S.ured[0];
-            for (int i = 1; i < WAVES; ++i) tup_merge(w, S.ured[i]);
-            TabUP* d = &XU[blockIdx.x];
-            if (w.idx >= row0 && w.idx < row1 && wave == (int)(w.pad >> 6)) {
-                const int wlr = wave * rw + (int)(w.pad & 63);
-                st_agent(&d->row[lane], C.ur[(int64_t)wlr * TKP + lane]);
-            }
+            lds_barrier();
             if (tid == 0) {
-                st_agent(&d->h.theta, w.theta);
-                st_agent(&d->h.idx, w.idx);
-                st_agent(&d->h.nonpos, w.nonpos);
-                st_agent(&d->h.T, w.T);
-                st_agent(&d->h.a_w, w.a_w);
-                st_agent(&d->h.cb_w, w.cb_w);
-                st_agent(&d->h.bix_w, w.bix_w);
+                UpdPartial w = S.ured[0];
+                for (int i = 1; i < WAVES; ++i) tup_merge(w, S.ured[i]);
+                UpdPartial* d = &XU[blockIdx.x];
+                st_agent(&d->theta, w.theta);
+                st_agent(&d->idx, w.idx);
+                st_agent(&d->nonpos, w.nonpos);
+                st_agent(&d->T, w.T);
+                st_agent(&d->a_w, w.a_w);
+                st_agent(&d->cb_w, w.cb_w);
+                st_agent(&d->bix_w, w.bix_w);
+                st_agent(&d->pad, w.pad);
             }
         }
+#if SPX_TAB_CLK == 3
+        if (clk) clk[2] = rtime();
+#endif
         target += (uint32_t)G;
         if (!grid_sync(La.ls, target, &s_ok)) return;
-#if SPX_TAB_CLK != 1
+#if SPX_TAB_CLK == 0 || SPX_TAB_CLK == 2
         if (clk) clk[2] = rtime();
 #endif
 
-        // ================= phase C: leaving row (all partials and eta rows in
-        // one round trip), s_y, bookkeeping (update_tail)
+        // ================= phase C: leaving row, s_y, bookkeeping (update_tail)
         {
             UpdPartial w = upd_empty();
-            double rowv[TPR];
-            if (pok) {
-                const TabUP* d = &XU[pg];
-                if (psub == 0) {
-                    w.theta = ld_agent(&d->h.theta);
-                    w.idx = ld_agent(&d->h.idx);
-                    w.nonpos = ld_agent(&d->h.nonpos);
-                    w.T = ld_agent(&d->h.T);
-                    w.a_w = ld_agent(&d->h.a_w);
-                    w.cb_w = ld_agent(&d->h.cb_w);
-                    w.bix_w = ld_agent(&d->h.bix_w);
-                    w.pad = pg;
-                }
-#pragma unroll
-                for (int k = 0; k < TPR; ++k)
-                    if (k < per && psub * per + k < TKW) rowv[k] = ld_agent(&d->row[psub * per + k]);
+            for (int g = tid; g < G; g += BLOCK) {
+                const UpdPartial* d = &XU[g];
+                w.theta = ld_agent(&d->theta);
+                w.idx = ld_agent(&d->idx);
+                w.nonpos = ld_agent(&d->nonpos);
+                w.T = ld_agent(&d->T);
+                w.a_w = ld_agent(&d->a_w);
+                w.cb_w = ld_agent(&d->cb_w);
+                w.bix_w = ld_agent(&d->bix_w);
+                w.pad = ld_agent(&d->pad);
             }
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
@@ -624,17 +712,19 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
                 w = lo;
             }
             if (lane == 0) S.ured[wave] = w;
-            __syncthreads();
-            UpdPartial t = S.ured[0];
-            for (int k2 = 1; k2 < WAVES; ++k2) tup_merge(t, S.ured[k2]);
-            // U[q][0..tau] of the new pending pivot, for the next pricing
-            if (pok && pg == (int)t.pad && t.idx >= 0 && t.idx < m) {
-#pragma unroll
-                for (int k = 0; k < TPR; ++k)
-                    if (k < per && psub * per + k < TKW) S.Uq[psub * per + k] = rowv[k];
+            lds_barrier();
+            if (tid == 0) {
+                UpdPartial t = S.ured[0];
+                for (int k2 = 1; k2 < WAVES; ++k2) tup_merge(t, S.ured[k2]);
+                S.uwin = t;
             }
-            if (tid == 0) S.uwin = t;
-            __syncthreads();
+            lds_barrier();
+            // U[q][0..tau] of the new pending pivot, for the next pricing:
+            // entries s < tau from earlier passes, entry tau from the partial
+            const int64_t qn = S.uwin.idx;
+            if (tid < KW)
+                S.Uq[tid] = (qn < 0 || qn >= m || tid >= nw) ? 0.0
+                          : (tid == tau ? __longlong_as_double(S.uwin.pad) : ld_agent(&P.U[qn * KW + tid]));
         }
         const UpdPartial t = S.uwin;
         if (t.nonpos == m || t.idx < 0 || t.idx >= m) {  // Unbounded (v4:319-322)
@@ -650,31 +740,20 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         const double s_y = y_scalar(t.T, aqn, t.cb_w, c_p);
         const int64_t kp = pw.slot;
         const double wp_new = P.devex ? ld_agent(&P.W[p]) : 0.0;
-        if (wg0 && tid == 0) {
-            if (kp != cnt - 1) {
-                st_agent(&P.nb_list[kp], (int32_t)lastv);
-                st_agent(&P.nb_pos[lastv], (int32_t)kp);
-            }
-            st_agent(&P.nb_pos[p], (int32_t)-1);
-            st_agent(&P.nb_list[cnt - 1], (int32_t)leave);
-            st_agent(&P.nb_pos[leave], (int32_t)(cnt - 1));
-            st_agent(&P.c_B[qn], c_p);
-            st_agent(&P.b_ixs[qn], p);
-            P.SY[nw] = s_y;
-            st->aq = aqn;
-            st->s_y = s_y;
-            st->nw = nw + 1;
-            st->xb_applied = it;
-            st->p = p;
-            st->q = qn;
-            st->min_e = P.devex ? pw.e : min_e;
-            st->iter = it + 1;
-            if (P.devex) {
-                st->leave = leave;
-                st->wp = wp_new;
-            }
-        }
-        if (wg0 && tid < nw) P.Urows[(int64_t)nw * KW + tid] = S.Uq[tid];
+        // the bookkeeping, written one phase later (flush)
+        bk = true;
+        bk_kp = kp;
+        bk_lastv = lastv;
+        bk_p = p;
+        bk_leave = leave;
+        bk_qn = qn;
+        bk_it = it;
+        bk_nw = nw;
+        bk_cp = c_p;
+        bk_sy = s_y;
+        bk_aq = aqn;
+        bk_mine = P.devex ? pw.e : min_e;
+        bk_wp = wp_new;
         if (rv && irow == qn) {  // the pivot's row: its basis entry (v4:339-342)
             bxr = p;
             cbr = c_p;
@@ -691,16 +770,18 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             if (h) {
                 rc_ls1 = lsn;
                 rc_j1 = leave;
+                rc_basic = pend ? ((qn == q) ? aq : 0.0) : 0.0;  // r_tau . A_leave, leave basic in row qn
             } else {
                 rc_ls0 = lsn;
                 rc_j0 = lastv;
             }
         }
         lastv = leave;
-        // the new pending pivot (tau' = nw): its base row into Qrows (this
-        // workgroup's slice)
-        for (int64_t k = qk0 + tid; k < qk1; k += BLOCK) P.Qrows[(int64_t)nw * L + k] = P.B0[qn * L + k];
+        // the new pending pivot (tau' = nw): its coefficients into Urows (k_fold)
+        if (wg0 && tid < nw) P.Urows[(int64_t)nw * KW + tid] = S.Uq[tid];
         if (tid == 0) S.SY[nw] = s_y;
+        q_prev = q;
+        aq_prev = aq;
         q = qn;
         aq = aqn;
         xb_applied = it;
@@ -708,8 +789,13 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         dwp = wp_new;
         ++nw;
         ++it;
-        __syncthreads();
+        lds_barrier();
     }
+    flush();
+    // the pending pivot's base row slice for k_fold (the next launch's
+    // prologue does not restage it)
+    if (nw > 0)
+        for (int64_t k = qk0 + tid; k < qk1; k += BLOCK) P.Qrows[(int64_t)(nw - 1) * L + k] = P.B0[q * L + k];
     if (wg0 && tid == 0) La.ls->passes = (int32_t)(it - it0);
 }
 
@@ -717,19 +803,18 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
 
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     if (!P.tab) return hipSuccess;
-    constexpr int TJ = 2;
-    const int64_t gy = (P.n + 64 * TJ - 1) / (64 * TJ);
-    // rows split so that the grid has about 2 workgroups per CU (8 waves)
+    const int64_t gy = (P.n + 63) / 64;
+    // rows split so that the grid has about 2 workgroups per CU (LDS: 68 KiB each)
     int64_t gx = (2 * (int64_t)cus + gy - 1) / gy;
-    const int64_t maxx = (P.m + 15) / 16;
+    const int64_t maxx = (P.m + TF_RB - 1) / TF_RB;
     if (gx > maxx) gx = maxx;
     if (gx < 1) gx = 1;
     const dim3 grid((unsigned)gx, (unsigned)gy);
     switch (P.win) {
-        case 8: hipLaunchKernelGGL((k_tab_fold<8, TJ>), grid, dim3(256), 0, s, P, min_nw); break;
-        case 16: hipLaunchKernelGGL((k_tab_fold<16, TJ>), grid, dim3(256), 0, s, P, min_nw); break;
-        case 32: hipLaunchKernelGGL((k_tab_fold<32, TJ>), grid, dim3(256), 0, s, P, min_nw); break;
-        case 64: hipLaunchKernelGGL((k_tab_fold<64, TJ>), grid, dim3(256), 0, s, P, min_nw); break;
+        case 8: hipLaunchKernelGGL(k_tab_fold<8>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_tab_fold<16>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_tab_fold<32>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_tab_fold<64>, grid, dim3(256), 0, s, P, min_nw); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -743,14 +828,6 @@ hipError_t launch_tab_build(const Params& P, hipStream_t s) {
 }
 
 constexpr int TAB_BLOCK = 512;
-
-// the instantiation whose per-thread partial-row slice covers G partials
-static const void* tab_loop_fn(int g) {
-    const int per = (TKW + TAB_BLOCK / g - 1) / (TAB_BLOCK / g);
-    if (per <= 8) return reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK, 8>);
-    if (per <= 16) return reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK, 16>);
-    return reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK, 32>);
-}
 
 hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c) {
     c.ok = false;
@@ -768,7 +845,7 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
         const int64_t r = ((P.m + g - 1) / g + W - 1) / W;
         cpw = (int)std::max<int64_t>(cp, 1);
         rw = (int)std::max<int64_t>(r, 1);
-        return cp <= 64 && r <= 64 && g <= TAB_BLOCK / 2 && TabCache<W>::bytes(cpw, rw) <= 150 * 1024;
+        return cp <= 64 && r <= 64 && TabCache<W>::bytes(cpw, rw) <= 150 * 1024;
     };
     int best = 0, cpw = 0, rw = 0;
     if (grid_hint > 0) {
@@ -792,11 +869,11 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
     e = hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
     if (e != hipSuccess) return e;
     if (!coop) return hipSuccess;
-    const void* fn = tab_loop_fn(best);
+    const void* fn = reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>);
     e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds_bytes);
     if (e != hipSuccess) return e;
     int per_cu = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TAB_BLOCK, c.lds_bytes);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tab_loop<TAB_BLOCK>, TAB_BLOCK, c.lds_bytes);
     if (e != hipSuccess) return e;
     c.ok = per_cu >= 1;
     return hipSuccess;
@@ -804,14 +881,14 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
 
 void tab_loop_partial_bytes(const LoopCfg& c, size_t* xp, size_t* xu) {
     *xp = sizeof(TabPP) * (size_t)c.grid;
-    *xu = sizeof(TabUP) * (size_t)c.grid;
+    *xu = sizeof(UpdPartial) * (size_t)c.grid;
 }
 
 hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s) {
     int cpw = c.cpw, rw = c.rw;
     void* args[] = {const_cast<Params*>(&P), const_cast<LoopArgs*>(&a), &cpw, &rw};
-    return hipLaunchCooperativeKernel(tab_loop_fn(c.grid), dim3(c.grid), dim3(c.block), args, (unsigned)c.lds_bytes,
-                                      s);
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(c.grid),
+                                      dim3(c.block), args, (unsigned)c.lds_bytes, s);
 }
 
 }  // namespace spx
