@@ -61,6 +61,8 @@ def parse():
                     help="B^-1 representation: 0 library default, -1 explicit rank-1 update, 8/16/32/64 eta window")
     ap.add_argument("--replicated", action="store_true",
                     help="N > 1: keep B^-1 replicated instead of row-sharded (SPX_FLAG_ROW_SHARD)")
+    ap.add_argument("--no-tableau", action="store_true",
+                    help="skip the window-tableau measurement (the `tableau` block, one GPU only)")
     ap.add_argument("--comm1", action="store_true",
                     help="rehearsal on one GPU: run the multi-rank path (torch.distributed + RCCL "
                          "MINLOC + row-sharded B^-1) with a one-rank communicator")
@@ -197,6 +199,10 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    tab = None
+    if world == 1 and not multi and not args.no_tableau:
+        tab = tableau_block(spx, torch, m, n, args, local)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(m, n, args.seed, args.cpu_seconds)
@@ -258,11 +264,66 @@ def main():
                 "throughput_GBps": price_bytes_all / (minloc_ms_max * 1e-3) / 1e9 if minloc_ms_max > 0 else 0.0,
                 "max_rank_update_ms": update_ms_max,
             },
+            "tableau": tab,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if multi:
         dist.destroy_process_group()
+
+
+def tableau_block(spx, torch, m, n, args, device):
+    """The same LP and pivot rule on the window tableau (SPX_FLAG_TABLEAU,
+    DESIGN.md §4d): T_w = B_w A and dw = y_w A - c are kept in HBM and folded
+    every 63 pivots by an fp64-MFMA rank-63 update, so a pivot reads neither
+    A nor B_w; the passes run in the persistent loop kernel (k_tab_loop).  Not
+    the north-star loop (no per-pivot A / B^-1 stream): reported beside it.
+    Timed like the headline (W warmup pivots, then K), plus an event-timed run
+    for the loop / fold split and the fold kernel's roofline."""
+    def run(timing):
+        with spx.Context(m=m, n=n, seed=args.seed, device=device, timing=timing, tableau=True) as ctx:
+            cfg = ctx.config()
+            ctx.iterate(args.warmup)
+            lt0 = ctx.loop_times() if timing else None
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, p0 = ctx.iterate(0)
+            _, p1 = ctx.iterate(args.steps)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            lt = ctx.loop_times() if timing else None
+            info = ctx.info()
+        return cfg, dt, p1 - p0, lt, info
+    cfg, dt, piv, _, info = run(False)
+    _, dt_e, piv_e, lt, _ = run(True)
+    L = info["ld"]
+    win = cfg["window"]
+    fold_bytes = 16.0 * L * n + 16.0 * m * L            # T_w and B_w read + written once per fold
+    fold_flops = 2.0 * m * (n + L) * (win - 1)          # rank-(KW-1) updates of T_w and B_w
+    folds = max(lt["folds"], 1)
+    fold_ms = lt["fold_ms"] / folds if lt["folds"] else 0.0
+    passes = max(lt["clock_passes"], 1)
+    out = {
+        "value": piv / dt if dt > 0 else 0.0,
+        "unit": "iterations/s",
+        "ms_per_step": 1e3 * dt / max(piv, 1),
+        "steps": piv,
+        "representation": f"window tableau {win}: T_w = B_w A, dw = y_w A - c in HBM, fp64-MFMA fold every "
+                          f"{win - 1} pivots; persistent loop kernel k_tab_loop ({cfg['loop_grid']} workgroups)"
+                          if cfg.get("persistent") else f"window tableau {win}, two-kernel passes",
+        "persistent": cfg.get("persistent", 0),
+        "loop": {"us_per_pass": 1e3 * lt["loop_ms"] / max(lt["loop_passes"], 1),
+                 "phase_us": {"pricing_to_barrier1": lt["price_us"] / passes,
+                              "ftran_ratio_to_barrier2": lt["ftran_us"] / passes,
+                              "leaving_row_bookkeeping": lt["tail_us"] / max(passes - 1, 1)}},
+        "fold": {"kernels": "k_tab_fold + k_fold", "avg_ms": fold_ms, "per_pivot_us": 1e3 * fold_ms / (win - 1),
+                 "algorithmic_bytes": fold_bytes, "flops": fold_flops,
+                 "achieved_GBps": fold_bytes / (fold_ms * 1e-3) / 1e9 if fold_ms > 0 else 0.0,
+                 "frac_hbm": fold_bytes / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if fold_ms > 0 else 0.0,
+                 "achieved_TFLOPs": fold_flops / (fold_ms * 1e-3) / 1e12 if fold_ms > 0 else 0.0},
+        "event_timed_ms_per_step": 1e3 * dt_e / max(piv_e, 1),
+    }
+    return out
 
 
 def glpk_status():

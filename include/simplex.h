@@ -273,8 +273,11 @@ int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
  * the passes they ran, since the last call; out[2..4] microseconds summed
  * over passes of the in-kernel phases seen by workgroup 0 (s_memrealtime):
  * pricing to grid barrier 1, FTRAN + ratio test to barrier 2, tail to the
- * next pass; passes = passes with a phase split.  Resets. */
-int spx_loop_times(spx_ctx* ctx, double out[5], int64_t* passes);
+ * next pass; passes = passes with a phase split; out[5] device milliseconds
+ * of the window folds launched between loop launches (hipEvents) and out[6]
+ * their count.  Resets. */
+#define SPX_LOOP_FIELDS 7
+int spx_loop_times(spx_ctx* ctx, double out[SPX_LOOP_FIELDS], int64_t* passes);
 
 /* Geometry and algorithmic bytes.  bytes_price: one pricing launch on this
  * rank (8*(m+1)*local non-basic columns), bytes_update: the B^-1 bytes per
@@ -289,8 +292,8 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * threads per workgroup, [5] update rows per wave, [6] update workgroups,
  * [7] passes per captured hipGraph (0 = eager), [8] persistent loop kernel
  * in use (1) or not (0), [9] its threads per workgroup, [10] window tableau
- * (SPX_FLAG_TABLEAU) in use. */
-#define SPX_CONFIG_FIELDS 11
+ * (SPX_FLAG_TABLEAU) in use, [11] workgroups of the persistent loop kernel. */
+#define SPX_CONFIG_FIELDS 12
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:

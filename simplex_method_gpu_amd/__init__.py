@@ -268,10 +268,10 @@ class Context:
     def loop_times(self):
         """Persistent loop kernel (timing=True): launch ms + passes (hipEvents)
         and the in-kernel phase split (microseconds summed over passes)."""
-        out, n = (ctypes.c_double * 5)(), ctypes.c_int64()
+        out, n = (ctypes.c_double * 7)(), ctypes.c_int64()
         check(self._L.spx_loop_times(self._h, out, ctypes.byref(n)))
         return {"loop_ms": out[0], "loop_passes": int(out[1]), "price_us": out[2], "ftran_us": out[3],
-                "tail_us": out[4], "clock_passes": n.value}
+                "tail_us": out[4], "clock_passes": n.value, "fold_ms": out[5], "folds": int(out[6])}
 
     def pass_times(self):
         """Event-timed sums (timing=True): pricing kernel, pricing + MINLOC
@@ -291,10 +291,10 @@ class Context:
 
     def config(self):
         """Resolved representation and launch geometry (spx_config)."""
-        out = (ctypes.c_int32 * 11)()
+        out = (ctypes.c_int32 * 12)()
         check(self._L.spx_config(self._h, out))
         keys = ("window", "price_block", "price_grid", "price_lds", "update_block", "update_rows", "update_grid",
-                "graph_batch", "persistent", "loop_block", "tableau")
+                "graph_batch", "persistent", "loop_block", "tableau", "loop_grid")
         return dict(zip(keys, list(out)))
 
 

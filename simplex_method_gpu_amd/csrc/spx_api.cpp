@@ -138,6 +138,8 @@ struct spx_ctx {
     std::vector<hipEvent_t> ev_loop;
     std::vector<int32_t> ev_loop_passes;
     size_t n_loop = 0;
+    std::vector<hipEvent_t> ev_fold;  // timing: the window folds between loop launches
+    size_t n_fold = 0;
 
     // basis reinversion (spx_reinv.h): work buffers allocated on first use
     RvParams rv{};
@@ -669,7 +671,22 @@ int iterate_persist(spx_ctx* x, int64_t k) {
     while (left > 0) {
         const bool fold = fold_due(x);
         if (fold) {
+            hipEvent_t f0 = nullptr, f1 = nullptr;
+            if (x->timing) {
+                if (x->ev_fold.size() < 2 * (x->n_fold + 1)) {
+                    for (int i = 0; i < 2; ++i) {
+                        hipEvent_t e;
+                        HIP_TRY(hipEventCreate(&e));
+                        x->ev_fold.push_back(e);
+                    }
+                }
+                f0 = x->ev_fold[2 * x->n_fold];
+                f1 = x->ev_fold[2 * x->n_fold + 1];
+                ++x->n_fold;
+                HIP_TRY(hipEventRecord(f0, x->stream));
+            }
             HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+            if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
             x->nw = 1;
         }
         const int64_t np = std::min<int64_t>(left, x->P.win - x->nw);
@@ -921,6 +938,8 @@ void spx_destroy(spx_ctx* x) {
     for (hipEvent_t e : x->ev_price) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_update) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_xend) (void)hipEventDestroy(e);
+    for (hipEvent_t e : x->ev_loop) (void)hipEventDestroy(e);
+    for (hipEvent_t e : x->ev_fold) (void)hipEventDestroy(e);
     if (x->comm) (void)ncclCommDestroy(x->comm);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->st_host) (void)hipHostFree(x->st_host);
@@ -1262,7 +1281,7 @@ int spx_pass_times(spx_ctx* x, double out[3], int64_t* passes) {
     return SPX_OK;
 }
 
-int spx_loop_times(spx_ctx* x, double out[5], int64_t* passes) {
+int spx_loop_times(spx_ctx* x, double out[SPX_LOOP_FIELDS], int64_t* passes) {
     if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
     HIP_TRY(hipStreamSynchronize(x->stream));
     double ms = 0.0;
@@ -1274,6 +1293,15 @@ int spx_loop_times(spx_ctx* x, double out[5], int64_t* passes) {
         np += x->ev_loop_passes[i];
     }
     x->n_loop = 0;
+    double fms = 0.0;
+    for (size_t i = 0; i < x->n_fold; ++i) {
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, x->ev_fold[2 * i], x->ev_fold[2 * i + 1]));
+        fms += t;
+    }
+    out[5] = fms;
+    out[6] = (double)x->n_fold;
+    x->n_fold = 0;
     out[0] = ms;
     out[1] = (double)np;
     out[2] = x->loop_clock[0];
@@ -1353,6 +1381,7 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[8] = x->persist ? 1 : 0;
     out[9] = x->persist ? x->lcfg.block : 0;
     out[10] = x->P.tab;
+    out[11] = x->persist ? x->lcfg.grid : 0;
     return SPX_OK;
 }
 
