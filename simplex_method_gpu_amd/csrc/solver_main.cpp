@@ -24,6 +24,8 @@
 //   --refactor K   rebuild B^-1 from the basis every K pivots (spx_reinvert)
 //   --window W     B^-1 representation (0 auto, -1 explicit, 8..64 eta window)
 //   --pricing P    entering-column rule: dantzig (v4:288-302, default) | devex
+//   --tableau      window tableau (SPX_FLAG_TABLEAU): T_w = B_w A
+//                  kept in HBM, no per-pivot A / B^-1 stream
 //   --mps          the input is an MPS file (mps_io.h): converted to the
 //                  canonical form (slacks, senses, bounds, big-M artificials)
 //                  and solved; output as the reference's GLPK driver
@@ -66,7 +68,7 @@ static void print_elapsed_time(const char* msg, double dur) {
 static void usage() {
     std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
                  " [--threads T] [--write-bin F] [--write-text F] [--no-solve] [--ratio reference|guarded|harris]"
-                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--pricing dantzig|devex]"
+                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--pricing dantzig|devex] [--tableau]"
                  " [--mps [--big-m M]]"
                  " (<file> | --gen m n seed)\n";
 }
@@ -85,7 +87,7 @@ int main(int argc, char* argv[]) {
     int ratio = -1, window = 0, pricing = SPX_PRICING_DANTZIG;
     double piv_tol = 1e-9, feas_tol = 1e-9, big_m = 0.0;
     int64_t refactor = 0;
-    bool mps_in = false;
+    bool mps_in = false, tableau = false;
     for (int a = 1; a < argc; ++a) {
         const std::string s = argv[a];
         auto need = [&](int k) {
@@ -118,6 +120,7 @@ int main(int argc, char* argv[]) {
         else if (s == "--refactor") { need(1); refactor = std::strtoll(argv[++a], nullptr, 10); }
         else if (s == "--window") { need(1); window = std::atoi(argv[++a]); }
         else if (s == "--mps") mps_in = true;
+        else if (s == "--tableau") tableau = true;
         else if (s == "--pricing") {
             need(1);
             const std::string r = argv[++a];
@@ -187,6 +190,7 @@ int main(int argc, char* argv[]) {
     o.refactor_every = (int32_t)refactor;
     o.window = window;
     o.pricing = pricing;
+    if (tableau) o.flags |= SPX_FLAG_TABLEAU;
     spx_ctx* ctx = nullptr;
     const TimePoint t_alloc = Clock::now();
     int rc = device_gen ? spx_create_generated(&ctx, m, n, gseed, &o)

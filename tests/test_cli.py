@@ -61,6 +61,20 @@ def test_generated_solve_json():
     assert js["status"] == 1 and abs(js["z"] - 115.9505237149796) < 1e-9 * 116
 
 
+@pytest.mark.gpu
+def test_generated_solve_tableau_json():
+    """--tableau (SPX_FLAG_TABLEAU): the same optimum and pivot count as the default run."""
+    import json
+
+    outs = []
+    for extra in ((), ("--tableau",)):
+        r = run("--no-iter-lines", "--json", *extra, "--gen", "300", "1200", "7")
+        assert r.returncode == 0, r.stderr
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[1]["status"] == outs[0]["status"] == 1
+    assert abs(outs[1]["z"] - outs[0]["z"]) <= 1e-9 * abs(outs[0]["z"])
+
+
 # --- LP file formats (SURVEY.md §8f row 3; simplex_method_gpu_amd/csrc/lp_io.h) ---
 
 def _numbers(path):
