@@ -8,6 +8,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "spx_device.h"
 
 namespace spx {
@@ -52,6 +54,80 @@ __device__ __forceinline__ void wave_sum2(double& a, double& b) {
         a += ta;
         b += tb;
     }
+}
+
+// ---- DPP cross-lane moves (gfx9 encodings; VALU-rate, no LDS round trip).
+// dpp_* returns v of the source lane the control selects, or old in lanes the
+// row mask leaves out.
+enum : int {
+    DPP_XOR1 = 0xB1,         // quad_perm [1,0,3,2]
+    DPP_XOR2 = 0x4E,         // quad_perm [2,3,0,1]
+    DPP_HALF_MIRROR = 0x141, // lane i <- 7 - i within 8
+    DPP_MIRROR = 0x140,      // lane i <- 15 - i within a row of 16
+    DPP_BCAST15 = 0x142,     // rows 1, 3 <- lane 15 of the row before (row mask 0xA)
+    DPP_BCAST31 = 0x143,     // rows 2, 3 <- lane 31 (row mask 0xC)
+};
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ int64_t dpp_l(int64_t old, int64_t v) {
+    const int lo = dpp_i<CTRL, RM>((int)old, (int)v);
+    const int hi = dpp_i<CTRL, RM>((int)(old >> 32), (int)(v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ double dpp_d(double old, double v) {
+    return __longlong_as_double(dpp_l<CTRL, RM>(__double_as_longlong(old), __double_as_longlong(v)));
+}
+// value of lane l (l wave-uniform) in every lane
+__device__ __forceinline__ int64_t readlane_l(int64_t v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    return __longlong_as_double(readlane_l(__double_as_longlong(v), l));
+}
+
+// Lane reductions in the pairing order of __shfl_xor offsets 1, 2, 4, ...:
+// the mirror and broadcast moves pair the same lane groups once each group
+// holds its own total, so a sum has the bits of that butterfly.  N = 8: every
+// lane of each aligned group of 8 ends with the group's result; N = 64: lane
+// 63 ends with the wave's (the other lanes hold partial results).
+template <int N, class Step>
+__device__ __forceinline__ void lane_reduce(Step step) {
+    static_assert(N == 8 || N == 64, "lane_reduce: 8 or 64 lanes");
+    step(std::integral_constant<int, DPP_XOR1>(), std::integral_constant<int, 0xF>());
+    step(std::integral_constant<int, DPP_XOR2>(), std::integral_constant<int, 0xF>());
+    step(std::integral_constant<int, DPP_HALF_MIRROR>(), std::integral_constant<int, 0xF>());
+    if constexpr (N == 64) {
+        step(std::integral_constant<int, DPP_MIRROR>(), std::integral_constant<int, 0xF>());
+        step(std::integral_constant<int, DPP_BCAST15>(), std::integral_constant<int, 0xA>());
+        step(std::integral_constant<int, DPP_BCAST31>(), std::integral_constant<int, 0xC>());
+    }
+}
+// (value, index) argmin with argmin_better's order (smallest index on ties)
+template <int N>
+__device__ __forceinline__ void lane_argmin(double& v, int64_t& j) {
+    lane_reduce<N>([&](auto c, auto rm) {
+        const double v2 = dpp_d<decltype(c)::value, decltype(rm)::value>(v, v);
+        const int64_t j2 = dpp_l<decltype(c)::value, decltype(rm)::value>(j, j);
+        if ((v2 < v) || (v2 == v && j2 < j)) {
+            v = v2;
+            j = j2;
+        }
+    });
+}
+template <int N>
+__device__ __forceinline__ void lane_sum(double& v) {
+    // lanes the row mask leaves out add old = 0.0
+    lane_reduce<N>([&](auto c, auto rm) { v += dpp_d<decltype(c)::value, decltype(rm)::value>(0.0, v); });
+}
+template <int N>
+__device__ __forceinline__ void lane_isum(int& v) {
+    lane_reduce<N>([&](auto c, auto rm) { v += dpp_i<decltype(c)::value, decltype(rm)::value>(0, v); });
 }
 
 template <typename T>

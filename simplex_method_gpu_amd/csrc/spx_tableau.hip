@@ -244,8 +244,15 @@ __global__ __launch_bounds__(256) void k_tab_build(Params P) {
 constexpr int TKW = 64;
 constexpr int TKP = TKW + 1;  // LDS row pitch (doubles): lane-per-row reads hit distinct banks
 #ifndef SPX_TAB_CLK
-#define SPX_TAB_CLK 0  // diagnostic stamp placement: 0 = phases A / B / C
+// diagnostic stamps of workgroup 0 (tools/tab_clk.sh): clk[0] = pass start,
+// clk[2] = barrier 2 done; clk[1] = barrier 1 done (0), or point k of the
+// pass (k = 1 .. 11, TAB_STAMP below) in a build with SPX_TAB_CLK = k
+#define SPX_TAB_CLK 0
 #endif
+#define TAB_STAMP(k)                                  \
+    do {                                              \
+        if (SPX_TAB_CLK == (k) && clk) clk[1] = rtime(); \
+    } while (0)
 
 struct alignas(16) TabPP {  // pricing partial: candidate, its window entry, its list slot
     double val;
@@ -265,26 +272,12 @@ struct TabPick {  // a pricing candidate being merged
 __device__ __forceinline__ void pick_merge(TabPick& a, const TabPick& b) {
     if (argmin_better(b.val, b.idx, a.val, a.idx)) a = b;
 }
-__device__ __forceinline__ TabPick pick_shfl_xor(const TabPick& v, int off) {
-    TabPick o;
-    o.val = __shfl_xor(v.val, off, 64);
-    o.idx = __shfl_xor(v.idx, off, 64);
-    o.w = __shfl_xor(v.w, off, 64);
-    o.e = __shfl_xor(v.e, off, 64);
-    o.slot = __shfl_xor(v.slot, off, 64);
-    return o;
-}
 
 // ratio-test merge carrying UpdPartial::pad (the winner's eta entry) with the winner
 __device__ __forceinline__ void tup_merge(UpdPartial& a, const UpdPartial& b) {
     const bool take = argmin_better(b.theta, b.idx, a.theta, a.idx);
     upd_merge(a, b);
     if (take) a.pad = b.pad;
-}
-__device__ __forceinline__ UpdPartial tup_shfl_xor(const UpdPartial& v, int off) {
-    UpdPartial o = upd_shfl_xor(v, off);
-    o.pad = __shfl_xor(v.pad, off, 64);
-    return o;
 }
 
 template <int WAVES>
@@ -294,8 +287,6 @@ struct TabLds {
     double Wp[TKW];
     TabPick ppick[WAVES];
     UpdPartial ured[WAVES];
-    TabPick pwin;
-    UpdPartial uwin;
 };
 
 // dynamic LDS: [W*cpw] int32 columns | [W*cpw] dw | [W*cpw] Devex weights |
@@ -372,10 +363,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     const int64_t qk1 = (qk0 + qsl < L) ? qk0 + qsl : L;
 
     // ---- prologue: window scalars, column and row caches
-    if (tid < KW) {
-        S.SY[tid] = (tid < nw) ? P.SY[tid] : 0.0;
-        S.Uq[tid] = (nw > 0 && tid < nw - 1) ? P.U[q * KW + tid] : 0.0;
-    }
+    if (tid < KW) S.SY[tid] = (tid < nw) ? P.SY[tid] : 0.0;
     if (nw > 0 && wg0 && tid < nw - 1) P.Urows[(int64_t)(nw - 1) * KW + tid] = P.U[q * KW + tid];
     if (cv) {
         const int32_t j = P.nb_list[vid + lane * stride];
@@ -409,6 +397,10 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     int rc_ls0 = -1, rc_ls1 = -1;
     int64_t rc_j0 = 0, rc_j1 = 0;
     double rc_basic = 0.0;  // the leaving column's window entry for the pivot that made it leave
+    // U[q][tau-1] of the pending pivot, from the ratio-test partial (its row
+    // owner's store is still in flight); false at launch: every entry is in HBM
+    bool uq_pad = false;
+    double uq_pad_v = 0.0;
     // results of a pass that go to HBM one phase later (after the next
     // barrier 1, so no barrier's drain waits for them): this lane's row
     // (eta entry, its basic column's window entry, x_b, alpha) and, in
@@ -465,42 +457,65 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         if (clk) clk[0] = rtime();
 
         // ================= phase A: pricing, lane c <-> column slot c
+        // Every load of the phase is issued before any is waited for (one
+        // round trip): the T_w row entry of this lane's column, the pending
+        // pivot's eta coefficients U[q][s<tau] (S.Uq), Wt[n][.] and xw[q]
+        // for s_x, this workgroup's slice of the base row B_w[q,:] (Qrows,
+        // stored in phase B) and the list slots the last pivot changed.
+        const int64_t cj = !cv ? 0 : (ls == rc_ls0) ? rc_j0 : (ls == rc_ls1) ? rc_j1 : (int64_t)C.col[ls];
+        const double tq = (pend && cv) ? P.T[cj * L + q] : 0.0;
+        double uqv = 0.0, wtn = 0.0;
+        if (pend && lane < tau) {
+            if (tid < KW) uqv = (uq_pad && lane == tau - 1) ? uq_pad_v : ld_agent(&P.U[q * KW + lane]);
+            wtn = ld_agent(&P.Wt[n * KW + lane]);
+        }
+        const double xwq = pend ? P.xw[q] : 0.0;
+        const double qv = (pend && qk0 + tid < qk1) ? P.B0[q * L + qk0 + tid] : 0.0;
         if (rc_ls0 >= 0 || rc_ls1 >= 0) {
+            double rw_v[2], rdw[2], rwc[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int lsn = h ? rc_ls1 : rc_ls0;
+                const int64_t jn = h ? rc_j1 : rc_j0;
+                rw_v[h] = rdw[h] = rwc[h] = 0.0;
+                if (lsn < 0) continue;
+                // the leaving column's entry for the last pivot: its basic-column
+                // value (stored one phase later, so not yet visible)
+                rw_v[h] = (h && lane == tau - 1) ? rc_basic : ((lane < tau) ? ld_agent(&P.Wt[jn * KW + lane]) : 0.0);
+                if (lane == 0) {
+                    rdw[h] = P.dw[jn];
+                    rwc[h] = P.devex ? ld_agent(&P.W[jn]) : 1.0;
+                }
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int lsn = h ? rc_ls1 : rc_ls0;
                 if (lsn < 0) continue;
-                const int64_t jn = h ? rc_j1 : rc_j0;
-                // the leaving column's entry for the last pivot: its basic-column
-                // value (stored one phase later, so not yet visible)
-                C.wt[(int64_t)lsn * TKP + lane] =
-                    (h && lane == tau - 1) ? rc_basic : ((lane < tau) ? ld_agent(&P.Wt[jn * KW + lane]) : 0.0);
+                C.wt[(int64_t)lsn * TKP + lane] = rw_v[h];
                 if (lane == 0) {
-                    C.col[lsn] = (int32_t)jn;
-                    C.dwc[lsn] = P.dw[jn];
-                    C.wc[lsn] = P.devex ? ld_agent(&P.W[jn]) : 1.0;
+                    C.col[lsn] = (int32_t)(h ? rc_j1 : rc_j0);
+                    C.dwc[lsn] = rdw[h];
+                    C.wc[lsn] = rwc[h];
                 }
             }
             rc_ls0 = rc_ls1 = -1;
         }
+        if (tid < KW) S.Uq[tid] = uqv;
+        // its coefficients into Urows (k_fold), as k_update stages them
+        if (pend && wg0 && tid < tau) P.Urows[(int64_t)tau * KW + tid] = uqv;
+        lds_barrier();
         // s_x = r_tau . b for phase B's x_b update (k_tab_update's formula)
         double sxw = 0.0;
-        if (pend) {
-            sxw = lane < tau ? S.Uq[lane] * ld_agent(&P.Wt[n * KW + lane]) : 0.0;
-            sxw = P.xw[q] + wave_sum(sxw);
-        }
+        if (pend) sxw = xwq + wave_sum(lane < tau ? S.Uq[lane] * wtn : 0.0);
+        TAB_STAMP(1);
         TabPick best{INFINITY, INT64_MAX, 0.0, 0.0, -1};
-        const int64_t cj = cv ? (int64_t)C.col[ls] : 0;
         double cw = 0.0, cwt = 0.0;  // this column's window entry and Devex weight, stored in phase B
         {
-            const double tq = (pend && cv) ? P.T[cj * L + q] : 0.0;
             const double dv = cv ? C.dwc[ls] : 0.0;
             const double* wrow = C.wt + (int64_t)ls * TKP;
             double e;
             tab_price_column(tq, dv, cv ? tau : -1, S.SY, S.Uq, [&](int s2) { return wrow[s2]; }, cw, e);
-#if SPX_TAB_CLK == 1  // diagnostic: {pass start, column done, barrier 1 done}
-            if (clk) clk[1] = rtime();
-#endif
+            TAB_STAMP(2);
             if (cv) {
                 if (pend) C.wt[(int64_t)ls * TKP + tau] = cw;
                 double key = e;
@@ -519,72 +534,76 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
                 best.val = key;
                 best.idx = cj;
             }
-            // wave argmin on (key, column); the winner's entry, reduced cost
-            // and slot come from its lane
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const double k2 = __shfl_xor(best.val, off, 64);
-                const int64_t j2 = __shfl_xor(best.idx, off, 64);
-                if (argmin_better(k2, j2, best.val, best.idx)) {
-                    best.val = k2;
-                    best.idx = j2;
-                }
-            }
-            const unsigned long long wb = __ballot(cv && cj == best.idx);
+            // wave argmin on (key, column) by DPP (lane 63 ends with it); the
+            // winner's entry, reduced cost and slot are read from its lane
+            double bv = best.val;
+            int64_t bj = best.idx;
+            lane_argmin<64>(bv, bj);
+            bv = readlane_d(bv, 63);
+            bj = readlane_l(bj, 63);
+            const unsigned long long wb = __ballot(cv && cj == bj);
             const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
-            best.w = __shfl(cw, wl, 64);
-            best.e = __shfl(e, wl, 64);
-            best.slot = (int64_t)vid + (int64_t)wl * stride;
+            best = TabPick{bv, bj, readlane_d(cw, wl), readlane_d(e, wl), (int64_t)vid + (int64_t)wl * stride};
         }
+        TAB_STAMP(3);
         if (lane == 0) S.ppick[wave] = best;
         lds_barrier();
-        if (tid == 0) {
-            TabPick w = S.ppick[0];
-            for (int i = 1; i < WAVES; ++i) pick_merge(w, S.ppick[i]);
-            TabPP* d = &XP[blockIdx.x];
-            st_agent(&d->val, w.val);
-            st_agent(&d->idx, w.idx);
-            st_agent(&d->w, w.w);
-            st_agent(&d->e, w.e);
-            st_agent(&d->slot, w.slot);
+        if (wave == 0) {  // workgroup merge: lane w holds wave w's pick; the winning lane stores the partial
+            const TabPick w = lane < WAVES ? S.ppick[lane] : TabPick{INFINITY, INT64_MAX, 0.0, 0.0, -1};
+            double bv = w.val;
+            int64_t bj = w.idx;
+            lane_argmin<8>(bv, bj);
+            bv = readlane_d(bv, 0);
+            bj = readlane_l(bj, 0);
+            const unsigned long long wb = __ballot(lane < WAVES && w.idx == bj && w.val == bv);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            if (lane == wl) {
+                TabPP* d = &XP[blockIdx.x];
+                st_agent(&d->val, w.val);
+                st_agent(&d->idx, w.idx);
+                st_agent(&d->w, w.w);
+                st_agent(&d->e, w.e);
+                st_agent(&d->slot, w.slot);
+            }
         }
+        TAB_STAMP(4);
         target += (uint32_t)G;
         if (!grid_sync(La.ls, target, &s_ok)) return;
-#if SPX_TAB_CLK == 0 || SPX_TAB_CLK == 1
-        if (clk) clk[SPX_TAB_CLK == 1 ? 2 : 1] = rtime();
-#endif
+        TAB_STAMP(0);
+        TAB_STAMP(5);
 
         // ================= phase B: entering column, FTRAN + ratio test
         // Deferred writes, drained at barrier 2: phase A's column results,
         // the last pass's row results and bookkeeping, and the pending
         // pivot's base row slice for k_fold.
-        if (cv && pend) {
-            st_agent(&P.Wt[cj * KW + tau], cw);
-            if (P.devex) st_agent(&P.W[cj], cwt);
-        }
-        if (pend && wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
-        flush();
-        if (pend)
-            for (int64_t k = qk0 + tid; k < qk1; k += BLOCK) P.Qrows[(int64_t)tau * L + k] = P.B0[q * L + k];
+        // Every wave reduces the pricing partials itself (same p everywhere,
+        // no LDS hand-off); they are loaded first, so their wait overlaps the
+        // stores.
+        TabPick pw;
         {
             TabPick w{INFINITY, INT64_MAX, 0.0, 0.0, -1};
-            for (int g = tid; g < G; g += BLOCK) {
+            for (int g = lane; g < G; g += 64) {
                 const TabPP* d = &XP[g];
-                w = TabPick{ld_agent(&d->val), ld_agent(&d->idx), ld_agent(&d->w), ld_agent(&d->e),
-                            ld_agent(&d->slot)};
+                pick_merge(w, TabPick{ld_agent(&d->val), ld_agent(&d->idx), ld_agent(&d->w), ld_agent(&d->e),
+                                      ld_agent(&d->slot)});
             }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) pick_merge(w, pick_shfl_xor(w, off));
-            if (lane == 0) S.ppick[wave] = w;
-            lds_barrier();
-            if (tid == 0) {
-                TabPick t = S.ppick[0];
-                for (int i = 1; i < WAVES; ++i) pick_merge(t, S.ppick[i]);
-                S.pwin = t;
+            if (cv && pend) {
+                st_agent(&P.Wt[cj * KW + tau], cw);
+                if (P.devex) st_agent(&P.W[cj], cwt);
             }
-            lds_barrier();
+            if (pend && wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
+            flush();
+            if (pend && qk0 + tid < qk1) P.Qrows[(int64_t)tau * L + qk0 + tid] = qv;
+            double bv = w.val;
+            int64_t bj = w.idx;
+            lane_argmin<64>(bv, bj);
+            bv = readlane_d(bv, 63);
+            bj = readlane_l(bj, 63);
+            const unsigned long long wb = __ballot(w.idx == bj && w.val == bv);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            pw = TabPick{bv, bj, readlane_d(w.w, wl), readlane_d(w.e, wl), readlane_l(w.slot, wl)};
         }
-        const TabPick pw = S.pwin;
+        TAB_STAMP(6);
         const int64_t p = pw.idx;
         const double min_e = pw.val;
         if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
@@ -596,6 +615,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             break;
         }
         double rei = 0.0;  // this lane's row: eta entry of the pending pivot
+        double c_p = 0.0;
         {
             // the entering column's window row: entries s < tau from earlier
             // passes, entry tau from its pricer's partial; a column that left
@@ -611,11 +631,10 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             }
             const bool upd_x = xb_applied < it;
             const double tcol = rv ? P.T[p * L + irow] : 0.0;
+            c_p = P.c[p];
             const double s_x = upd_x ? sxw : 0.0;
             lds_barrier();
-#if SPX_TAB_CLK == 2  // diagnostic: {pass start, barrier 1 done, p and Wt[p] known}
-            if (clk) clk[1] = rtime();
-#endif
+            TAB_STAMP(7);
             double th = INFINITY, tT = 0.0, a = 0.0;
             int64_t ti = INT64_MAX;
             if (rv) {
@@ -637,96 +656,94 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
                 r_bx = bxr;
                 r_bv = (irow == q) ? aq : 0.0;  // r_tau . A_j of the basic column j of this row
             }
-#if SPX_TAB_CLK == 3  // diagnostic: {pass start, FTRAN rows done, partial written}
-            if (clk) clk[1] = rtime();
-#endif
-            // wave merge: argmin on (theta, row) and the c_B.alpha sum
-            // together; alpha <= 0 counted by ballot; the winner's scalars
-            // (and its eta entry, U[q][tau] for the next pricing) from its lane
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const double t2 = __shfl_xor(th, off, 64);
-                const int64_t i2 = __shfl_xor(ti, off, 64);
-                tT += __shfl_xor(tT, off, 64);
-                if (argmin_better(t2, i2, th, ti)) {
-                    th = t2;
-                    ti = i2;
-                }
-            }
-            UpdPartial wp = upd_empty();
-            wp.theta = th;
-            wp.idx = ti;
-            wp.T = tT;
+            TAB_STAMP(8);
+            // wave merge by DPP: argmin on (theta, row) and the c_B.alpha sum;
+            // alpha <= 0 counted by ballot; the winner's scalars (and its eta
+            // entry, U[q][tau] for the next pricing) from its lane
+            double bth = th;
+            int64_t bti = ti;
+            lane_argmin<64>(bth, bti);
+            lane_sum<64>(tT);
+            UpdPartial wp;
+            wp.theta = readlane_d(bth, 63);
+            wp.idx = readlane_l(bti, 63);
+            wp.T = readlane_d(tT, 63);
             wp.nonpos = __popcll(__ballot(rv && !(a > P.piv_tol)));
-            const unsigned long long wb = __ballot(rv && irow == ti);
+            const unsigned long long wb = __ballot(rv && irow == wp.idx);
             const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
-            wp.a_w = __shfl(a, wl, 64);
-            wp.cb_w = __shfl(cbr, wl, 64);
-            wp.bix_w = __shfl(bxr, wl, 64);
-            wp.pad = __double_as_longlong(__shfl(rei, wl, 64));
+            wp.a_w = readlane_d(a, wl);
+            wp.cb_w = readlane_d(cbr, wl);
+            wp.bix_w = readlane_l(bxr, wl);
+            wp.pad = readlane_l(__double_as_longlong(rei), wl);
             if (lane == 0) S.ured[wave] = wp;
             lds_barrier();
-            if (tid == 0) {
-                UpdPartial w = S.ured[0];
-                for (int i = 1; i < WAVES; ++i) tup_merge(w, S.ured[i]);
-                UpdPartial* d = &XU[blockIdx.x];
-                st_agent(&d->theta, w.theta);
-                st_agent(&d->idx, w.idx);
-                st_agent(&d->nonpos, w.nonpos);
-                st_agent(&d->T, w.T);
-                st_agent(&d->a_w, w.a_w);
-                st_agent(&d->cb_w, w.cb_w);
-                st_agent(&d->bix_w, w.bix_w);
-                st_agent(&d->pad, w.pad);
+            if (wave == 0) {  // workgroup merge: lane w holds wave w's partial
+                const UpdPartial u = lane < WAVES ? S.ured[lane] : upd_empty();
+                double uth = u.theta, uT = u.T;
+                int64_t uti = u.idx;
+                int unp = (int)u.nonpos;
+                lane_argmin<8>(uth, uti);
+                lane_sum<8>(uT);
+                lane_isum<8>(unp);
+                uth = readlane_d(uth, 0);
+                uti = readlane_l(uti, 0);
+                const int64_t snp = __builtin_amdgcn_readlane(unp, 0);
+                const double sT = readlane_d(uT, 0);  // (cross-lane reads stay outside the branch)
+                const unsigned long long wb2 = __ballot(lane < WAVES && u.idx == uti && u.theta == uth);
+                const int wl2 = wb2 ? __ffsll((long long)wb2) - 1 : 0;
+                if (lane == wl2) {
+                    UpdPartial* d = &XU[blockIdx.x];
+                    st_agent(&d->theta, u.theta);
+                    st_agent(&d->idx, u.idx);
+                    st_agent(&d->nonpos, snp);
+                    st_agent(&d->T, sT);
+                    st_agent(&d->a_w, u.a_w);
+                    st_agent(&d->cb_w, u.cb_w);
+                    st_agent(&d->bix_w, u.bix_w);
+                    st_agent(&d->pad, u.pad);
+                }
             }
         }
-#if SPX_TAB_CLK == 3
-        if (clk) clk[2] = rtime();
-#endif
+        TAB_STAMP(9);
         target += (uint32_t)G;
         if (!grid_sync(La.ls, target, &s_ok)) return;
-#if SPX_TAB_CLK == 0 || SPX_TAB_CLK == 2
         if (clk) clk[2] = rtime();
-#endif
 
         // ================= phase C: leaving row, s_y, bookkeeping (update_tail)
-        {
+        UpdPartial t;
+        {  // every wave reduces the ratio-test partials itself (DPP; no LDS hand-off)
             UpdPartial w = upd_empty();
-            for (int g = tid; g < G; g += BLOCK) {
+            for (int g = lane; g < G; g += 64) {
                 const UpdPartial* d = &XU[g];
-                w.theta = ld_agent(&d->theta);
-                w.idx = ld_agent(&d->idx);
-                w.nonpos = ld_agent(&d->nonpos);
-                w.T = ld_agent(&d->T);
-                w.a_w = ld_agent(&d->a_w);
-                w.cb_w = ld_agent(&d->cb_w);
-                w.bix_w = ld_agent(&d->bix_w);
-                w.pad = ld_agent(&d->pad);
+                UpdPartial v;
+                v.theta = ld_agent(&d->theta);
+                v.idx = ld_agent(&d->idx);
+                v.nonpos = ld_agent(&d->nonpos);
+                v.T = ld_agent(&d->T);
+                v.a_w = ld_agent(&d->a_w);
+                v.cb_w = ld_agent(&d->cb_w);
+                v.bix_w = ld_agent(&d->bix_w);
+                v.pad = ld_agent(&d->pad);
+                tup_merge(w, v);
             }
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const UpdPartial o = tup_shfl_xor(w, off);
-                UpdPartial lo = (lane & off) ? o : w;
-                const UpdPartial hi = (lane & off) ? w : o;
-                tup_merge(lo, hi);
-                w = lo;
-            }
-            if (lane == 0) S.ured[wave] = w;
-            lds_barrier();
-            if (tid == 0) {
-                UpdPartial t = S.ured[0];
-                for (int k2 = 1; k2 < WAVES; ++k2) tup_merge(t, S.ured[k2]);
-                S.uwin = t;
-            }
-            lds_barrier();
-            // U[q][0..tau] of the new pending pivot, for the next pricing:
-            // entries s < tau from earlier passes, entry tau from the partial
-            const int64_t qn = S.uwin.idx;
-            if (tid < KW)
-                S.Uq[tid] = (qn < 0 || qn >= m || tid >= nw) ? 0.0
-                          : (tid == tau ? __longlong_as_double(S.uwin.pad) : ld_agent(&P.U[qn * KW + tid]));
+            double bth = w.theta, sT = w.T;
+            int64_t bti = w.idx;
+            int np = (int)w.nonpos;
+            lane_argmin<64>(bth, bti);
+            lane_sum<64>(sT);
+            lane_isum<64>(np);
+            t.theta = readlane_d(bth, 63);
+            t.idx = readlane_l(bti, 63);
+            t.T = readlane_d(sT, 63);
+            t.nonpos = __builtin_amdgcn_readlane(np, 63);
+            const unsigned long long wb = __ballot(w.idx == t.idx && w.theta == t.theta);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            t.a_w = readlane_d(w.a_w, wl);
+            t.cb_w = readlane_d(w.cb_w, wl);
+            t.bix_w = readlane_l(w.bix_w, wl);
+            t.pad = readlane_l(w.pad, wl);
         }
-        const UpdPartial t = S.uwin;
+        TAB_STAMP(10);
         if (t.nonpos == m || t.idx < 0 || t.idx >= m) {  // Unbounded (v4:319-322)
             if (wg0 && tid == 0) {
                 st->p = p;
@@ -736,7 +753,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             break;
         }
         const int64_t qn = t.idx, leave = t.bix_w;
-        const double aqn = t.a_w, c_p = P.c[p];
+        const double aqn = t.a_w;
         const double s_y = y_scalar(t.T, aqn, t.cb_w, c_p);
         const int64_t kp = pw.slot;
         const double wp_new = P.devex ? ld_agent(&P.W[p]) : 0.0;
@@ -777,8 +794,10 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             }
         }
         lastv = leave;
-        // the new pending pivot (tau' = nw): its coefficients into Urows (k_fold)
-        if (wg0 && tid < nw) P.Urows[(int64_t)nw * KW + tid] = S.Uq[tid];
+        // the new pending pivot's eta coefficient U[qn][tau] (the next
+        // phase A loads the entries s < tau)
+        uq_pad = true;
+        uq_pad_v = __longlong_as_double(t.pad);
         if (tid == 0) S.SY[nw] = s_y;
         q_prev = q;
         aq_prev = aq;
@@ -789,6 +808,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         dwp = wp_new;
         ++nw;
         ++it;
+        TAB_STAMP(11);
         lds_barrier();
     }
     flush();
@@ -845,7 +865,8 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
         const int64_t r = ((P.m + g - 1) / g + W - 1) / W;
         cpw = (int)std::max<int64_t>(cp, 1);
         rw = (int)std::max<int64_t>(r, 1);
-        return cp <= 64 && r <= 64 && TabCache<W>::bytes(cpw, rw) <= 150 * 1024;
+        const int64_t qsl = ((P.L + g - 1) / g + 1) / 2 * 2;  // Qrows slice: one element per thread
+        return cp <= 64 && r <= 64 && qsl <= TAB_BLOCK && g <= TAB_BLOCK && TabCache<W>::bytes(cpw, rw) <= 150 * 1024;
     };
     int best = 0, cpw = 0, rw = 0;
     if (grid_hint > 0) {
