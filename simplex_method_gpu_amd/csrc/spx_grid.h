@@ -19,9 +19,10 @@ __device__ __forceinline__ bool grid_sync(LoopState* ls, uint32_t target, int* s
         const uint32_t old = __hip_atomic_fetch_add(&ls->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1 < target) {
             uint32_t spins = 0;
+            // one load in flight per poll; the error word and the spin
+            // bound are checked every 256 polls only
             while (ld_agent(&ls->bar) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 24) || ld_agent(&ls->err)) {
+                if ((++spins & 255u) == 0 && (spins > (1u << 24) || ld_agent(&ls->err))) {
                     st_agent(&ls->err, 1);
                     ok = 0;
                     break;

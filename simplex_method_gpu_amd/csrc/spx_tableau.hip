@@ -254,14 +254,26 @@ constexpr int TKP = TKW + 1;  // LDS row pitch (doubles): lane-per-row reads hit
         if (SPX_TAB_CLK == (k) && clk) clk[1] = rtime(); \
     } while (0)
 
-struct alignas(16) TabPP {  // pricing partial: candidate, its window entry, its list slot
-    double val;
-    int64_t idx;
-    double w;
-    double e;
-    int64_t slot;
-    int64_t pad;
-};
+// Cross-workgroup partials, stored field-major (word f of workgroup g at
+// [f * G + g]) so that a wave reading all G of one field touches G * 8
+// contiguous bytes.  Pricing: val, idx, w, e, slot; ratio test: the
+// UpdPartial fields in declaration order.
+constexpr int TAB_PP_FIELDS = 5;
+constexpr int TAB_UP_FIELDS = 8;
+template <typename T>
+__device__ __forceinline__ void st_word(uint64_t* base, int f, int G, int g, T v) {
+    static_assert(sizeof(T) == 8, "8-byte partial words");
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    st_agent(&base[(int64_t)f * G + g], u);
+}
+template <typename T>
+__device__ __forceinline__ T ld_word(const uint64_t* base, int f, int G, int g) {
+    const uint64_t u = ld_agent(&base[(int64_t)f * G + g]);
+    T v;
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+}
 
 struct TabPick {  // a pricing candidate being merged
     double val;
@@ -319,8 +331,8 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     __shared__ int s_ok;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TabCache<WAVES> C(smem, cpw);
-    TabPP* const XP = reinterpret_cast<TabPP*>(La.xp);
-    UpdPartial* const XU = reinterpret_cast<UpdPartial*>(La.xu);
+    uint64_t* const XP = reinterpret_cast<uint64_t*>(La.xp);
+    uint64_t* const XU = reinterpret_cast<uint64_t*>(La.xu);
     DevState* st = P.st;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -558,12 +570,12 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             const unsigned long long wb = __ballot(lane < WAVES && w.idx == bj && w.val == bv);
             const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
             if (lane == wl) {
-                TabPP* d = &XP[blockIdx.x];
-                st_agent(&d->val, w.val);
-                st_agent(&d->idx, w.idx);
-                st_agent(&d->w, w.w);
-                st_agent(&d->e, w.e);
-                st_agent(&d->slot, w.slot);
+                const int g = blockIdx.x;
+                st_word(XP, 0, G, g, w.val);
+                st_word(XP, 1, G, g, w.idx);
+                st_word(XP, 2, G, g, w.w);
+                st_word(XP, 3, G, g, w.e);
+                st_word(XP, 4, G, g, w.slot);
             }
         }
         TAB_STAMP(4);
@@ -582,11 +594,10 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         TabPick pw;
         {
             TabPick w{INFINITY, INT64_MAX, 0.0, 0.0, -1};
-            for (int g = lane; g < G; g += 64) {
-                const TabPP* d = &XP[g];
-                pick_merge(w, TabPick{ld_agent(&d->val), ld_agent(&d->idx), ld_agent(&d->w), ld_agent(&d->e),
-                                      ld_agent(&d->slot)});
-            }
+            for (int g = lane; g < G; g += 64)
+                pick_merge(w, TabPick{ld_word<double>(XP, 0, G, g), ld_word<int64_t>(XP, 1, G, g),
+                                      ld_word<double>(XP, 2, G, g), ld_word<double>(XP, 3, G, g),
+                                      ld_word<int64_t>(XP, 4, G, g)});
             if (cv && pend) {
                 st_agent(&P.Wt[cj * KW + tau], cw);
                 if (P.devex) st_agent(&P.W[cj], cwt);
@@ -692,15 +703,15 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
                 const unsigned long long wb2 = __ballot(lane < WAVES && u.idx == uti && u.theta == uth);
                 const int wl2 = wb2 ? __ffsll((long long)wb2) - 1 : 0;
                 if (lane == wl2) {
-                    UpdPartial* d = &XU[blockIdx.x];
-                    st_agent(&d->theta, u.theta);
-                    st_agent(&d->idx, u.idx);
-                    st_agent(&d->nonpos, snp);
-                    st_agent(&d->T, sT);
-                    st_agent(&d->a_w, u.a_w);
-                    st_agent(&d->cb_w, u.cb_w);
-                    st_agent(&d->bix_w, u.bix_w);
-                    st_agent(&d->pad, u.pad);
+                    const int g = blockIdx.x;
+                    st_word(XU, 0, G, g, u.theta);
+                    st_word(XU, 1, G, g, u.idx);
+                    st_word(XU, 2, G, g, snp);
+                    st_word(XU, 3, G, g, sT);
+                    st_word(XU, 4, G, g, u.a_w);
+                    st_word(XU, 5, G, g, u.cb_w);
+                    st_word(XU, 6, G, g, u.bix_w);
+                    st_word(XU, 7, G, g, u.pad);
                 }
             }
         }
@@ -714,16 +725,15 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         {  // every wave reduces the ratio-test partials itself (DPP; no LDS hand-off)
             UpdPartial w = upd_empty();
             for (int g = lane; g < G; g += 64) {
-                const UpdPartial* d = &XU[g];
                 UpdPartial v;
-                v.theta = ld_agent(&d->theta);
-                v.idx = ld_agent(&d->idx);
-                v.nonpos = ld_agent(&d->nonpos);
-                v.T = ld_agent(&d->T);
-                v.a_w = ld_agent(&d->a_w);
-                v.cb_w = ld_agent(&d->cb_w);
-                v.bix_w = ld_agent(&d->bix_w);
-                v.pad = ld_agent(&d->pad);
+                v.theta = ld_word<double>(XU, 0, G, g);
+                v.idx = ld_word<int64_t>(XU, 1, G, g);
+                v.nonpos = ld_word<int64_t>(XU, 2, G, g);
+                v.T = ld_word<double>(XU, 3, G, g);
+                v.a_w = ld_word<double>(XU, 4, G, g);
+                v.cb_w = ld_word<double>(XU, 5, G, g);
+                v.bix_w = ld_word<int64_t>(XU, 6, G, g);
+                v.pad = ld_word<int64_t>(XU, 7, G, g);
                 tup_merge(w, v);
             }
             double bth = w.theta, sT = w.T;
@@ -901,8 +911,8 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
 }
 
 void tab_loop_partial_bytes(const LoopCfg& c, size_t* xp, size_t* xu) {
-    *xp = sizeof(TabPP) * (size_t)c.grid;
-    *xu = sizeof(UpdPartial) * (size_t)c.grid;
+    *xp = 8 * TAB_PP_FIELDS * (size_t)c.grid;
+    *xu = 8 * TAB_UP_FIELDS * (size_t)c.grid;
 }
 
 hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s) {
