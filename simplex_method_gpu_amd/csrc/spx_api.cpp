@@ -135,6 +135,7 @@ struct spx_ctx {
     bool persist = false;
     double loop_clock[3] = {0.0, 0.0, 0.0};  // timing: phase A / B / C microseconds (in-kernel clock)
     int64_t loop_clock_passes = 0;
+    uint32_t loop_epoch = 0;  // persistent launches so far (LoopArgs::epoch)
     std::vector<hipEvent_t> ev_loop;
     std::vector<int32_t> ev_loop_passes;
     size_t n_loop = 0;
@@ -434,6 +435,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
             unsigned char *xp = nullptr, *xu = nullptr;
             SPX_TRY(x->alloc(&xp, xpb));
             SPX_TRY(x->alloc(&xu, xub));
+            // tagged partial words (spx_tableau.hip): no tag matches 0xFF..
+            HIP_TRY(hipMemset(xp, 0xFF, xpb));
+            HIP_TRY(hipMemset(xu, 0xFF, xub));
             x->la.xp = xp;
             x->la.xu = xu;
             SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
@@ -692,6 +696,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
         const int64_t np = std::min<int64_t>(left, x->P.win - x->nw);
         LoopArgs a = x->la;
         a.npasses = (int32_t)np;
+        a.epoch = ++x->loop_epoch & 0x1ffffffu;  // 25 bits: the tag keeps 7 for pass and phase
         if (!x->timing) a.clock = nullptr;
         HIP_TRY(hipMemsetAsync(a.ls, 0, sizeof(LoopState), x->stream));
         hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -41,9 +41,9 @@ struct LoopArgs {
     LoopState* ls;
     unsigned long long* clock;  // optional: per pass {start, barrier 1, barrier 2} (s_memrealtime), WG 0
     int32_t npasses;            // passes to run (the window must not fill)
-    int32_t pad;
-    void* xp;                   // tableau loop: G pricing partials with the candidate's window row
-    void* xu;                   // tableau loop: G ratio-test partials with the candidate's eta row
+    uint32_t epoch;             // tableau loop: launch number (tags of the partial words)
+    void* xp;                   // tableau loop: G tagged pricing partials (spx_tableau.hip)
+    void* xu;                   // tableau loop: G tagged ratio-test partials
 };
 
 struct LoopCfg {

@@ -19,7 +19,6 @@
 
 #include "spx_common.h"
 #include "spx_fold.h"
-#include "spx_grid.h"
 #include "spx_loop.h"
 #include "spx_tableau.h"
 #include "spx_tabdev.h"
@@ -254,25 +253,71 @@ constexpr int TKP = TKW + 1;  // LDS row pitch (doubles): lane-per-row reads hit
         if (SPX_TAB_CLK == (k) && clk) clk[1] = rtime(); \
     } while (0)
 
-// Cross-workgroup partials, stored field-major (word f of workgroup g at
-// [f * G + g]) so that a wave reading all G of one field touches G * 8
-// contiguous bytes.  Pricing: val, idx, w, e, slot; ratio test: the
-// UpdPartial fields in declaration order.
+// Cross-workgroup partials without a grid barrier.  Each 8-byte field of a
+// workgroup's partial travels as two tagged words, (tag << 32) | 32-bit half,
+// stored field-major (word k of workgroup g at [k * G + g], so a wave reading
+// word k of all G touches G * 8 contiguous bytes).  An aligned 8-byte store
+// is single-copy atomic, so a reader that sees the current tag in every word
+// of a partial has all of it; it polls the words until then.  The tag is
+// unique per launch and exchange: (epoch << 7) | (pass << 1) | phase, epoch
+// the host's launch counter (the buffers start as 0xFF..: no tag matches).
+// Data that crosses workgroups beside the partials (the phase-B deferred
+// writes: Wt entries, U entries, Devex weights) is stored agent-scope, and
+// every wave drains (s_waitcnt vmcnt(0)) before its workgroup publishes the
+// ratio-test partial: whoever has read all ratio-test partials of a pass sees
+// those writes (MI355X_MICROARCH.md's hand-off rule, with the tag as flag).
+// Pricing partial: val, idx, w, e, slot; ratio test: the UpdPartial fields.
 constexpr int TAB_PP_FIELDS = 5;
 constexpr int TAB_UP_FIELDS = 8;
-template <typename T>
-__device__ __forceinline__ void st_word(uint64_t* base, int f, int G, int g, T v) {
-    static_assert(sizeof(T) == 8, "8-byte partial words");
-    uint64_t u;
-    __builtin_memcpy(&u, &v, 8);
-    st_agent(&base[(int64_t)f * G + g], u);
+__device__ __forceinline__ uint32_t tab_tag(uint32_t epoch, int pass, int phase) {
+    return (epoch << 7) | ((uint32_t)pass << 1) | (uint32_t)phase;
 }
 template <typename T>
-__device__ __forceinline__ T ld_word(const uint64_t* base, int f, int G, int g) {
-    const uint64_t u = ld_agent(&base[(int64_t)f * G + g]);
+__device__ __forceinline__ void st_tagged(uint64_t* X, int f, int G, int g, uint32_t tag, T v) {
+    static_assert(sizeof(T) == 8, "8-byte partial fields");
+    uint64_t u;
+    __builtin_memcpy(&u, &v, 8);
+    const uint64_t t = (uint64_t)tag << 32;
+    st_agent(&X[(int64_t)(2 * f) * G + g], (uint64_t)(t | (u & 0xffffffffull)));
+    st_agent(&X[(int64_t)(2 * f + 1) * G + g], (uint64_t)(t | (u >> 32)));
+}
+template <typename T>
+__device__ __forceinline__ T tagged_field(const uint64_t* w, int f) {
+    const uint64_t u = (uint64_t)((w[2 * f] & 0xffffffffull) | (w[2 * f + 1] << 32));
     T v;
     __builtin_memcpy(&v, &u, 8);
     return v;
+}
+// Wave-wide poll (one wave per workgroup polls): every lane with g < G
+// watches word 0 of workgroup g's partial until it carries tag, then loads
+// all 2 NF words (again until all carry it; normally once).  false: the poll
+// timed out (err is set).
+template <int NF>
+__device__ __forceinline__ bool poll_tagged(const uint64_t* X, int G, int g, uint32_t tag, uint64_t (&w)[2 * NF],
+                                            LoopState* ls) {
+    uint32_t spins = 0;
+    for (;;) {
+        const bool ok = g >= G || (uint32_t)(ld_agent(&X[g]) >> 32) == tag;
+        if (__ballot(!ok) == 0) break;
+        if ((++spins & 255u) == 0 && (spins > (1u << 22) || ld_agent(&ls->err))) {
+            st_agent(&ls->err, 1);
+            return false;
+        }
+    }
+    for (;;) {
+        bool ok = true;
+        if (g < G) {
+#pragma unroll
+            for (int k = 0; k < 2 * NF; ++k) w[k] = ld_agent(&X[(int64_t)k * G + g]);
+#pragma unroll
+            for (int k = 0; k < 2 * NF; ++k) ok = ok && (uint32_t)(w[k] >> 32) == tag;
+        }
+        if (__ballot(!ok) == 0) return true;
+        if ((++spins & 255u) == 0 && (spins > (1u << 22) || ld_agent(&ls->err))) {
+            st_agent(&ls->err, 1);
+            return false;
+        }
+    }
 }
 
 struct TabPick {  // a pricing candidate being merged
@@ -299,6 +344,9 @@ struct TabLds {
     double Wp[TKW];
     TabPick ppick[WAVES];
     UpdPartial ured[WAVES];
+    TabPick pwin;
+    UpdPartial uwin;
+    int fail;
 };
 
 // dynamic LDS: [W*cpw] int32 columns | [W*cpw] dw | [W*cpw] Devex weights |
@@ -328,7 +376,6 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int cpw, int rw) {
     constexpr int WAVES = BLOCK / 64;
     __shared__ TabLds<WAVES> S;
-    __shared__ int s_ok;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TabCache<WAVES> C(smem, cpw);
     uint64_t* const XP = reinterpret_cast<uint64_t*>(La.xp);
@@ -403,7 +450,6 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         C.ur[(int64_t)(wave * rw + r) * TKP + lane] = (lane < nw - 1) ? P.U[i * KW + lane] : 0.0;
     }
     lds_barrier();
-    uint32_t target = 0;
     // list slots the last pivot changed, owned by this wave: re-cached at the
     // start of the next pricing phase (their window rows then are visible)
     int rc_ls0 = -1, rc_ls1 = -1;
@@ -569,42 +615,45 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             bj = readlane_l(bj, 0);
             const unsigned long long wb = __ballot(lane < WAVES && w.idx == bj && w.val == bv);
             const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
-            if (lane == wl) {
+            if (lane == wl) {  // no drain: phase A stores nothing another workgroup reads
                 const int g = blockIdx.x;
-                st_word(XP, 0, G, g, w.val);
-                st_word(XP, 1, G, g, w.idx);
-                st_word(XP, 2, G, g, w.w);
-                st_word(XP, 3, G, g, w.e);
-                st_word(XP, 4, G, g, w.slot);
+                const uint32_t tg = tab_tag(La.epoch, pass, 0);
+                st_tagged(XP, 0, G, g, tg, w.val);
+                st_tagged(XP, 1, G, g, tg, w.idx);
+                st_tagged(XP, 2, G, g, tg, w.w);
+                st_tagged(XP, 3, G, g, tg, w.e);
+                st_tagged(XP, 4, G, g, tg, w.slot);
             }
         }
         TAB_STAMP(4);
-        target += (uint32_t)G;
-        if (!grid_sync(La.ls, target, &s_ok)) return;
-        TAB_STAMP(0);
         TAB_STAMP(5);
 
         // ================= phase B: entering column, FTRAN + ratio test
         // Deferred writes, drained at barrier 2: phase A's column results,
         // the last pass's row results and bookkeeping, and the pending
         // pivot's base row slice for k_fold.
-        // Every wave reduces the pricing partials itself (same p everywhere,
-        // no LDS hand-off); they are loaded first, so their wait overlaps the
-        // stores.
-        TabPick pw;
-        {
+        // Wave 0 polls the pricing partials and reduces them (the same p in
+        // every workgroup); the other waves meanwhile issue the deferred
+        // stores, then read the result from LDS.
+        if (cv && pend) {
+            st_agent(&P.Wt[cj * KW + tau], cw);
+            if (P.devex) st_agent(&P.W[cj], cwt);
+        }
+        if (pend && wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
+        flush();
+        if (pend && qk0 + tid < qk1) P.Qrows[(int64_t)tau * L + qk0 + tid] = qv;
+        if (wave == 0) {
             TabPick w{INFINITY, INT64_MAX, 0.0, 0.0, -1};
-            for (int g = lane; g < G; g += 64)
-                pick_merge(w, TabPick{ld_word<double>(XP, 0, G, g), ld_word<int64_t>(XP, 1, G, g),
-                                      ld_word<double>(XP, 2, G, g), ld_word<double>(XP, 3, G, g),
-                                      ld_word<int64_t>(XP, 4, G, g)});
-            if (cv && pend) {
-                st_agent(&P.Wt[cj * KW + tau], cw);
-                if (P.devex) st_agent(&P.W[cj], cwt);
+            const uint32_t tg = tab_tag(La.epoch, pass, 0);
+            bool ok = true;
+            for (int g0 = 0; g0 < G && ok; g0 += 64) {
+                uint64_t x[2 * TAB_PP_FIELDS];
+                ok = poll_tagged<TAB_PP_FIELDS>(XP, G, g0 + lane, tg, x, La.ls);
+                if (ok && g0 + lane < G)
+                    pick_merge(w, TabPick{tagged_field<double>(x, 0), tagged_field<int64_t>(x, 1),
+                                          tagged_field<double>(x, 2), tagged_field<double>(x, 3),
+                                          tagged_field<int64_t>(x, 4)});
             }
-            if (pend && wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
-            flush();
-            if (pend && qk0 + tid < qk1) P.Qrows[(int64_t)tau * L + qk0 + tid] = qv;
             double bv = w.val;
             int64_t bj = w.idx;
             lane_argmin<64>(bv, bj);
@@ -612,9 +661,17 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             bj = readlane_l(bj, 63);
             const unsigned long long wb = __ballot(w.idx == bj && w.val == bv);
             const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
-            pw = TabPick{bv, bj, readlane_d(w.w, wl), readlane_d(w.e, wl), readlane_l(w.slot, wl)};
+            const TabPick r{bv, bj, readlane_d(w.w, wl), readlane_d(w.e, wl), readlane_l(w.slot, wl)};
+            if (lane == 0) {
+                S.pwin = r;
+                S.fail = !ok;
+            }
         }
-        TAB_STAMP(6);
+        lds_barrier();
+        if (S.fail) return;
+        const TabPick pw = S.pwin;
+        TAB_STAMP(0);
+        TAB_STAMP(5);
         const int64_t p = pw.idx;
         const double min_e = pw.val;
         if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
@@ -687,6 +744,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             wp.bix_w = readlane_l(bxr, wl);
             wp.pad = readlane_l(__double_as_longlong(rei), wl);
             if (lane == 0) S.ured[wave] = wp;
+            drain_vmem();  // this pass's agent-scope writes, before the partial publishes them
             lds_barrier();
             if (wave == 0) {  // workgroup merge: lane w holds wave w's partial
                 const UpdPartial u = lane < WAVES ? S.ured[lane] : upd_empty();
@@ -704,55 +762,69 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
                 const int wl2 = wb2 ? __ffsll((long long)wb2) - 1 : 0;
                 if (lane == wl2) {
                     const int g = blockIdx.x;
-                    st_word(XU, 0, G, g, u.theta);
-                    st_word(XU, 1, G, g, u.idx);
-                    st_word(XU, 2, G, g, snp);
-                    st_word(XU, 3, G, g, sT);
-                    st_word(XU, 4, G, g, u.a_w);
-                    st_word(XU, 5, G, g, u.cb_w);
-                    st_word(XU, 6, G, g, u.bix_w);
-                    st_word(XU, 7, G, g, u.pad);
+                    const uint32_t tg = tab_tag(La.epoch, pass, 1);
+                    st_tagged(XU, 0, G, g, tg, u.theta);
+                    st_tagged(XU, 1, G, g, tg, u.idx);
+                    st_tagged(XU, 2, G, g, tg, snp);
+                    st_tagged(XU, 3, G, g, tg, sT);
+                    st_tagged(XU, 4, G, g, tg, u.a_w);
+                    st_tagged(XU, 5, G, g, tg, u.cb_w);
+                    st_tagged(XU, 6, G, g, tg, u.bix_w);
+                    st_tagged(XU, 7, G, g, tg, u.pad);
                 }
             }
         }
         TAB_STAMP(9);
-        target += (uint32_t)G;
-        if (!grid_sync(La.ls, target, &s_ok)) return;
-        if (clk) clk[2] = rtime();
 
         // ================= phase C: leaving row, s_y, bookkeeping (update_tail)
-        UpdPartial t;
-        {  // every wave reduces the ratio-test partials itself (DPP; no LDS hand-off)
-            UpdPartial w = upd_empty();
-            for (int g = lane; g < G; g += 64) {
-                UpdPartial v;
-                v.theta = ld_word<double>(XU, 0, G, g);
-                v.idx = ld_word<int64_t>(XU, 1, G, g);
-                v.nonpos = ld_word<int64_t>(XU, 2, G, g);
-                v.T = ld_word<double>(XU, 3, G, g);
-                v.a_w = ld_word<double>(XU, 4, G, g);
-                v.cb_w = ld_word<double>(XU, 5, G, g);
-                v.bix_w = ld_word<int64_t>(XU, 6, G, g);
-                v.pad = ld_word<int64_t>(XU, 7, G, g);
-                tup_merge(w, v);
+        {  // wave 0 polls the ratio-test partials and reduces them (DPP)
+            if (wave == 0) {
+                UpdPartial w = upd_empty();
+                const uint32_t tg = tab_tag(La.epoch, pass, 1);
+                bool ok = true;
+                for (int g0 = 0; g0 < G && ok; g0 += 64) {
+                    uint64_t x[2 * TAB_UP_FIELDS];
+                    ok = poll_tagged<TAB_UP_FIELDS>(XU, G, g0 + lane, tg, x, La.ls);
+                    if (ok && g0 + lane < G) {
+                        UpdPartial v;
+                        v.theta = tagged_field<double>(x, 0);
+                        v.idx = tagged_field<int64_t>(x, 1);
+                        v.nonpos = tagged_field<int64_t>(x, 2);
+                        v.T = tagged_field<double>(x, 3);
+                        v.a_w = tagged_field<double>(x, 4);
+                        v.cb_w = tagged_field<double>(x, 5);
+                        v.bix_w = tagged_field<int64_t>(x, 6);
+                        v.pad = tagged_field<int64_t>(x, 7);
+                        tup_merge(w, v);
+                    }
+                }
+                if (clk) clk[2] = rtime();
+                double bth = w.theta, sT = w.T;
+                int64_t bti = w.idx;
+                int np = (int)w.nonpos;
+                lane_argmin<64>(bth, bti);
+                lane_sum<64>(sT);
+                lane_isum<64>(np);
+                UpdPartial r;
+                r.theta = readlane_d(bth, 63);
+                r.idx = readlane_l(bti, 63);
+                r.T = readlane_d(sT, 63);
+                r.nonpos = __builtin_amdgcn_readlane(np, 63);
+                const unsigned long long wb = __ballot(w.idx == r.idx && w.theta == r.theta);
+                const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+                r.a_w = readlane_d(w.a_w, wl);
+                r.cb_w = readlane_d(w.cb_w, wl);
+                r.bix_w = readlane_l(w.bix_w, wl);
+                r.pad = readlane_l(w.pad, wl);
+                if (lane == 0) {
+                    S.uwin = r;
+                    S.fail = !ok;
+                }
             }
-            double bth = w.theta, sT = w.T;
-            int64_t bti = w.idx;
-            int np = (int)w.nonpos;
-            lane_argmin<64>(bth, bti);
-            lane_sum<64>(sT);
-            lane_isum<64>(np);
-            t.theta = readlane_d(bth, 63);
-            t.idx = readlane_l(bti, 63);
-            t.T = readlane_d(sT, 63);
-            t.nonpos = __builtin_amdgcn_readlane(np, 63);
-            const unsigned long long wb = __ballot(w.idx == t.idx && w.theta == t.theta);
-            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
-            t.a_w = readlane_d(w.a_w, wl);
-            t.cb_w = readlane_d(w.cb_w, wl);
-            t.bix_w = readlane_l(w.bix_w, wl);
-            t.pad = readlane_l(w.pad, wl);
+            lds_barrier();
+            if (S.fail) return;
         }
+        const UpdPartial t = S.uwin;
         TAB_STAMP(10);
         if (t.nonpos == m || t.idx < 0 || t.idx >= m) {  // Unbounded (v4:319-322)
             if (wg0 && tid == 0) {
@@ -911,8 +983,8 @@ hipError_t tab_loop_prepare(const Params& P, int cus, int grid_hint, LoopCfg& c)
 }
 
 void tab_loop_partial_bytes(const LoopCfg& c, size_t* xp, size_t* xu) {
-    *xp = 8 * TAB_PP_FIELDS * (size_t)c.grid;
-    *xu = 8 * TAB_UP_FIELDS * (size_t)c.grid;
+    *xp = 16 * TAB_PP_FIELDS * (size_t)c.grid;
+    *xu = 16 * TAB_UP_FIELDS * (size_t)c.grid;
 }
 
 hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s) {
