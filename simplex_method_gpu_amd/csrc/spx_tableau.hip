@@ -862,10 +862,11 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         // the start of the next pricing phase
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int64_t slot = h ? (int64_t)cnt - 1 : kp;
+            const int slot = h ? cnt - 1 : (int)kp;  // the list holds n - m < 2^31 entries
             if (h == 0 && kp == cnt - 1) continue;
-            if ((int)(slot % stride) != vid) continue;
-            const int lsn = wave * cpw + (int)(slot / stride);
+            const int sq = slot / stride;
+            if (slot - sq * stride != vid) continue;
+            const int lsn = wave * cpw + sq;
             if (h) {
                 rc_ls1 = lsn;
                 rc_j1 = leave;
