@@ -1304,12 +1304,13 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
 // Eta-window fold (spx_device.h): B_w += U[:, 0..nf) R, y_w += SY[0..nf) R for
 // the nf = nw - 1 complete pivots of the window; the pending pivot stays
 // pending as tau = 0.  A workgroup owns a 64-column stripe of B and a range of
-// rows.  Wave 0 rebuilds R for the stripe (one column per lane:
-// r_tau = Qrows[tau] + sum_{s<tau} Urows[tau][s] r_s) into LDS; then each wave
-// updates 16-row x 64-column tiles with v_mfma_f64_16x16x4_f64 (K = the
-// window, 4 pivots per step): the tile of B is the accumulator, U the A
-// operand, R the B operand.  B is read and written once.  min_nw: fold only
-// when nw >= min_nw (the loop asks for KW, a readback for 2).
+// rows (spx_fold.h): its first tiles go in flight, wave 0 rebuilds R for the
+// stripe (one column per lane: r_tau = Qrows[tau] + sum_{s<tau} Urows[tau][s]
+// r_s) into LDS; then each wave updates 16-row x 64-column tiles with
+// v_mfma_f64_16x16x4_f64 (K = the window, 4 pivots per step): the tile of B is
+// the accumulator, U the A operand, R the B operand.  B is read and written
+// once.  min_nw: fold only when nw >= min_nw (the loop asks for KW, a readback
+// for 2).
 // ---------------------------------------------------------------------------
 template <int KW>
 __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
@@ -1318,14 +1319,19 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
     __shared__ double Rl[KW][64];
+    __shared__ double NT[KW][FOLD_NP<KW>];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t L = P.L;
     const int64_t c0 = (int64_t)blockIdx.x * 64;
+    int64_t i0, i1;
+    fold_rows(P.m, i0, i1);
+    fold_stage_N<KW>(P.Urows, nf, NT);
+    __syncthreads();
     if (wave == 0) {
         double R[KW];
-        fold_rebuild_R<KW>(P.Qrows, P.Urows, nf, L, c0, Rl, R);
+        fold_rebuild_R<KW>(P.Qrows, NT, nf, L, c0, Rl, R);
         if (blockIdx.y == 0) {
             double* y = st->y_buf ? P.y1 : P.y0;
             double d = 0.0;
@@ -1334,16 +1340,15 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
                 if (t < nf) d = fma(P.SY[t], R[t], d);
             y[c0 + lane] += d;
         }
-    }
-    __syncthreads();
-    const int64_t m = P.m;
-    const int64_t per = ((m + gridDim.y - 1) / gridDim.y + 15) / 16 * 16;
-    const int64_t i0 = (int64_t)blockIdx.y * per;
-    const int64_t i1 = (i0 + per < m) ? i0 + per : m;
-    fold_tiles<KW>(P.B0, P.U, nf, L, c0, i0, i1, Rl);
-    if (blockIdx.x == 0) {  // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf)
+    } else if (wave == 1) {
+        // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf); the rows
+        // spread over every workgroup, one lane per row, t ascending
         const double* wb = P.Wt + P.n * KW;
-        for (int64_t i = i0 + tid; i < i1; i += 256) {
+        const int64_t nwg = (int64_t)gridDim.x * gridDim.y;
+        const int64_t rpw = (P.m + nwg - 1) / nwg;
+        const int64_t r0 = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * rpw;
+        const int64_t r1 = (r0 + rpw < P.m) ? r0 + rpw : P.m;
+        for (int64_t i = r0 + lane; i < r1; i += 64) {
             double d = 0.0;
 #pragma unroll
             for (int t = 0; t < KW; ++t)
@@ -1351,6 +1356,8 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
             P.xw[i] += d;
         }
     }
+    __syncthreads();
+    fold_tiles<KW>(P.B0, P.U, nf, L, c0, i0, i1, Rl);
     __syncthreads();
     if (tid == 0) {
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket_fold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1630,11 +1637,7 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
         if (e != hipSuccess) return e;
     }
     const int nx = (int)(P.L / 64);
-    int64_t ny = ((int64_t)4 * cus + nx - 1) / nx;
-    const int64_t maxy = (P.m + 63) / 64;  // at least one 16-row tile per wave
-    if (ny > maxy) ny = maxy;
-    if (ny < 1) ny = 1;
-    const dim3 grid((unsigned)nx, (unsigned)ny);
+    const dim3 grid((unsigned)nx, (unsigned)fold_grid_y(P.m, nx, cus));
     switch (P.win) {
         case 8: hipLaunchKernelGGL(k_fold<8>, grid, dim3(256), 0, s, P, min_nw); break;
         case 16: hipLaunchKernelGGL(k_fold<16>, grid, dim3(256), 0, s, P, min_nw); break;

@@ -195,17 +195,18 @@ __global__ __launch_bounds__(256) void k_rv_step(RvParams R, int tau, const doub
 __global__ __launch_bounds__(256) void k_rv_fold(RvParams R) {
     if (R.rs->singular) return;
     __shared__ double Rl[RV_NB][64];
+    __shared__ double NT[RV_NB][FOLD_NP<RV_NB>];
     const int64_t L = R.L;
     const int64_t c0 = (int64_t)blockIdx.x * 64;
+    int64_t i0, i1;
+    fold_rows(R.m, i0, i1);
+    fold_stage_N<RV_NB>(R.Urows, R.nb, NT);
+    __syncthreads();
     if ((threadIdx.x >> 6) == 0) {
         double Rr[RV_NB];
-        fold_rebuild_R<RV_NB>(R.Qrows, R.Urows, R.nb, L, c0, Rl, Rr);
+        fold_rebuild_R<RV_NB>(R.Qrows, NT, R.nb, L, c0, Rl, Rr);
     }
     __syncthreads();
-    const int64_t m = R.m;
-    const int64_t per = ((m + gridDim.y - 1) / gridDim.y + 15) / 16 * 16;
-    const int64_t i0 = (int64_t)blockIdx.y * per;
-    const int64_t i1 = (i0 + per < m) ? i0 + per : m;
     fold_tiles<RV_NB>(R.X, R.U, R.nb, L, c0, i0, i1, Rl);
 }
 
@@ -311,11 +312,7 @@ hipError_t rv_launch_step(const RvParams& R, int tau, const double* Pin, double*
 
 hipError_t rv_launch_fold(const RvParams& R, int cus, hipStream_t s) {
     const int nx = (int)(R.L / 64);
-    int64_t ny = ((int64_t)4 * cus + nx - 1) / nx;
-    const int64_t maxy = (R.m + 63) / 64;
-    if (ny > maxy) ny = maxy;
-    if (ny < 1) ny = 1;
-    hipLaunchKernelGGL(k_rv_fold, dim3((unsigned)nx, (unsigned)ny), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(k_rv_fold, dim3((unsigned)nx, (unsigned)fold_grid_y(R.m, nx, cus)), dim3(256), 0, s, R);
     return hipGetLastError();
 }
 
