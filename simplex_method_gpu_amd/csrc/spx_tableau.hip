@@ -28,29 +28,35 @@ namespace spx {
 namespace {
 
 // ---------------------------------------------------------------------------
-// T_w += U Wt^T, dw += SY Wt^T.  A workgroup (4 waves) owns 64 columns of T_w
-// and a range of rows, walked 64 rows at a time.  Wave w keeps the Wt
-// fragments of its 16 columns in registers (MFMA A operand, lane:
-// Wt[j0 + cl][4 s + kr]).  The eta rows U[i0 .. i0+64) of a block — 32 KiB,
-// contiguous — are staged once per workgroup into LDS with 16-byte loads
+// T_w += U Wt^T, dw += SY Wt^T.  A workgroup (TF_WAVES waves) owns 16
+// TF_WAVES columns of T_w and a range of rows, walked 64 rows at a time.  Wave
+// w keeps the Wt fragments of its 16 columns in registers (MFMA A operand,
+// lane: Wt[j0 + cl][4 s + kr]).  The eta rows U[i0 .. i0+64) of a block — 32
+// KiB, contiguous — are staged once per workgroup into LDS with 16-byte loads
 // (double-buffered: the next block's are loaded before this block's MFMAs)
 // and read from there as the B operand (lane: U[i + cl][4 s + kr]).  The 4
 // accumulator tiles of a wave (lane: T_w[i + 16 it + cl, j0 + kr + 4 r]) are
-// T_w itself, read and written once; the next block's tiles are also in
-// flight during this block's 4 x ceil(nf/4) v_mfma_f64_16x16x4f64.
+// T_w itself, read and written once; the next block's tiles are loaded after
+// this block's stores (holding them across the MFMAs cost 32 VGPRs and
+// measured slower).  8 waves sharing one U staging, 120 VGPRs, 2 workgroups
+// per CU: 320 -> 260 us at C3 (tools/fold_bench.hip, MALL flushed),
+// bit-identical (the per-element MFMA chain is unchanged).
 // ---------------------------------------------------------------------------
+constexpr int TF_WAVES = 8;
+constexpr int TF_BLOCK = 64 * TF_WAVES;
 constexpr int TF_RB = 64;  // rows per block
 constexpr int TF_UP = 68;  // LDS pitch of a staged eta row (doubles): 16-B aligned, spreads banks
 
 template <int KW>
-__global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
+__global__ __launch_bounds__(TF_BLOCK) void k_tab_fold(Params P, int min_nw) {
     const DevState* st = P.st;
     const int nw = st->nw;
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
     constexpr int KS = KW / 4;
     constexpr int KW2 = KW / 2;             // dbl2 per eta row
-    constexpr int UPT = TF_RB * KW2 / 256;  // dbl2 staged per thread per block
+    constexpr int NST = TF_RB * KW2;                       // dbl2 staged per block
+    constexpr int UPT = (NST + TF_BLOCK - 1) / TF_BLOCK;  // per thread (KW = 8: half the threads)
     __shared__ __attribute__((aligned(16))) double Ub[2][TF_RB * TF_UP];
     const int ks = (nf + 3) / 4;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -60,9 +66,9 @@ __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
     const double* __restrict__ U = P.U;
     const double* __restrict__ Wt = P.Wt;
     double* __restrict__ T = P.T;
-    const int64_t cb = (int64_t)blockIdx.y * 64;  // this workgroup's columns
+    const int64_t cb = (int64_t)blockIdx.y * 16 * TF_WAVES;  // this workgroup's columns
 
-    if (blockIdx.x == 0 && tid < 64 && cb + tid < n) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t]
+    if (blockIdx.x == 0 && tid < 16 * TF_WAVES && cb + tid < n) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t]
         const int64_t j = cb + tid;
         double d = 0.0;
         for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
@@ -87,16 +93,16 @@ __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
     auto stage_load = [&](int64_t i0, dbl2 (&ur)[UPT]) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int pce = tid + 256 * k;
+            const int pce = tid + TF_BLOCK * k;
             const int64_t i = i0 + pce / KW2;
-            ur[k] = (i < i_hi) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
+            ur[k] = (pce < NST && i < i_hi) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
         }
     };
     auto stage_write = [&](int buf, const dbl2 (&ur)[UPT]) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
-            const int pce = tid + 256 * k;
-            *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * TF_UP + 2 * (pce % KW2)]) = ur[k];
+            const int pce = tid + TF_BLOCK * k;
+            if (pce < NST) *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * TF_UP + 2 * (pce % KW2)]) = ur[k];
         }
     };
     auto tile_load = [&](int64_t i0, dbl4 (&acc)[4]) {
@@ -118,11 +124,7 @@ __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
     int buf = 0;
     for (int64_t i0 = i_lo; i0 < i_hi; i0 += TF_RB, buf ^= 1) {
         const bool more = i0 + TF_RB < i_hi;
-        dbl4 nxt[4];
-        if (more) {
-            stage_load(i0 + TF_RB, ur);
-            tile_load(i0 + TF_RB, nxt);
-        }
+        if (more) stage_load(i0 + TF_RB, ur);
         const double* ub = Ub[buf];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -145,8 +147,7 @@ __global__ __launch_bounds__(256) void k_tab_fold(Params P, int min_nw) {
         }
         if (more) {
             stage_write(buf ^ 1, ur);
-#pragma unroll
-            for (int it = 0; it < 4; ++it) acc[it] = nxt[it];
+            tile_load(i0 + TF_RB, acc);
         }
         __syncthreads();
     }
@@ -906,7 +907,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
 
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     if (!P.tab) return hipSuccess;
-    const int64_t gy = (P.n + 63) / 64;
+    const int64_t gy = (P.n + 16 * TF_WAVES - 1) / (16 * TF_WAVES);
     // rows split so that the grid has about 2 workgroups per CU (LDS: 68 KiB each)
     int64_t gx = (2 * (int64_t)cus + gy - 1) / gy;
     const int64_t maxx = (P.m + TF_RB - 1) / TF_RB;
@@ -914,10 +915,10 @@ hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) 
     if (gx < 1) gx = 1;
     const dim3 grid((unsigned)gx, (unsigned)gy);
     switch (P.win) {
-        case 8: hipLaunchKernelGGL(k_tab_fold<8>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 16: hipLaunchKernelGGL(k_tab_fold<16>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 32: hipLaunchKernelGGL(k_tab_fold<32>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 64: hipLaunchKernelGGL(k_tab_fold<64>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 8: hipLaunchKernelGGL(k_tab_fold<8>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_tab_fold<16>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_tab_fold<32>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_tab_fold<64>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

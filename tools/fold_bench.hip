@@ -499,6 +499,115 @@ __global__ __launch_bounds__(256) void k_tab_fold_valu(TPar P, int nf, int cpw) 
     }
 }
 
+// Variants of the shipped tableau fold: WAVES waves per workgroup (16 columns
+// each, so 16 WAVES columns per workgroup), NBUF LDS buffers of staged U rows,
+// PF = next block's T tiles in flight during this block's MFMAs.
+template <int KW, int WAVES, int NBUF, bool PF>
+__global__ __launch_bounds__(64 * WAVES) void k_tab_fold_v(TPar P, int min_nw) {
+    constexpr int BLK = 64 * WAVES;
+    const FakeSt* st = P.st;
+    const int nw = st->nw;
+    if (nw < min_nw || nw < 2) return;
+    const int nf = nw - 1;
+    constexpr int KS = KW / 4;
+    constexpr int KW2 = KW / 2;
+    constexpr int UPT = TF_RB * KW2 / BLK;
+    __shared__ __attribute__((aligned(16))) double Ub[NBUF][TF_RB * TF_UP];
+    const int ks = (nf + 3) / 4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cl = lane & 15, kr = lane >> 4;
+    const int64_t m = P.m, n = P.n, L = P.L;
+    const double* __restrict__ U = P.U;
+    const double* __restrict__ Wt = P.Wt;
+    double* __restrict__ T = P.T;
+    const int64_t cb = (int64_t)blockIdx.y * 16 * WAVES;
+    const int64_t per = ((m + gridDim.x - 1) / gridDim.x + TF_RB - 1) / TF_RB * TF_RB;
+    const int64_t i_lo = (int64_t)blockIdx.x * per;
+    const int64_t i_hi = (i_lo + per < m) ? i_lo + per : m;
+    if (cb >= n || i_lo >= i_hi) return;
+    const int64_t j0 = cb + 16 * wave;
+    double wf[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int t = 4 * s + kr;
+        wf[s] = (j0 + cl < n && t < nf) ? Wt[(j0 + cl) * KW + t] : 0.0;
+    }
+    bool jok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) jok[r] = j0 + kr + 4 * r < n;
+    auto stage_load = [&](int64_t i0, dbl2(&ur)[UPT]) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int pce = tid + BLK * k;
+            const int64_t i = i0 + pce / KW2;
+            ur[k] = (i < i_hi) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
+        }
+    };
+    auto stage_write = [&](int buf, const dbl2(&ur)[UPT]) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            const int pce = tid + BLK * k;
+            *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * TF_UP + 2 * (pce % KW2)]) = ur[k];
+        }
+    };
+    auto tile_load = [&](int64_t i0, dbl4(&acc)[4]) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int64_t i = i0 + 16 * it + cl;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[it][r] = (jok[r] && i < i_hi) ? T[(j0 + kr + 4 * r) * L + i] : 0.0;
+        }
+    };
+    dbl2 ur[UPT];
+    dbl4 acc[4];
+    stage_load(i_lo, ur);
+    tile_load(i_lo, acc);
+    stage_write(0, ur);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t i0 = i_lo; i0 < i_hi; i0 += TF_RB) {
+        const bool more = i0 + TF_RB < i_hi;
+        dbl4 nxt[4];
+        if (more) {
+            stage_load(i0 + TF_RB, ur);
+            if (PF) tile_load(i0 + TF_RB, nxt);
+        }
+        const double* ub = Ub[buf];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s < ks) {
+#pragma unroll
+                for (int it = 0; it < 4; ++it) {
+                    const double bv = ub[(16 * it + cl) * TF_UP + 4 * s + kr];
+                    acc[it] = __builtin_amdgcn_mfma_f64_16x16x4f64(wf[s], bv, acc[it], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int64_t i = i0 + 16 * it + cl;
+            if (i < i_hi) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (jok[r]) T[(j0 + kr + 4 * r) * L + i] = acc[it][r];
+            }
+        }
+        if (more) {
+            if (NBUF == 1) __syncthreads();  // every wave is done reading Ub[0]
+            stage_write(NBUF == 1 ? 0 : (buf ^ 1), ur);
+            if (PF) {
+#pragma unroll
+                for (int it = 0; it < 4; ++it) acc[it] = nxt[it];
+            } else {
+                tile_load(i0 + TF_RB, acc);
+            }
+        }
+        if (NBUF == 2) buf ^= 1;
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_flush_mall(const double* f, long n, double* sink) {
     double a = 0.0;
     for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long)gridDim.x * 256) a += f[k];
@@ -646,6 +755,24 @@ int main(int argc, char** argv) {
         const long gy = (n + 63) / 64;
         long gx = (2 * 256 + gy - 1) / gy;
         tf("tab fold mfma (shipped)", [&] { hipLaunchKernelGGL(k_tab_fold_mfma<KW>, dim3(gx, gy), dim3(256), 0, 0, P, 2); });
+        auto tv = [&](const char* name, auto kern, int waves, int per_cu) {
+            const long gyv = (n + 16 * waves - 1) / (16 * waves);
+            long gxv = ((long)per_cu * 256 + gyv - 1) / gyv;
+            const long maxx = (m + 63) / 64;
+            if (gxv > maxx) gxv = maxx;
+            tf(name, [&] { hipLaunchKernelGGL(kern, dim3(gxv, gyv), dim3(64 * waves), 0, 0, P, 2); });
+        };
+        tv("tv W4 B2 PF (=shipped) 2/CU", k_tab_fold_v<KW, 4, 2, true>, 4, 2);
+        tv("tv W4 B2 PF 4/CU", k_tab_fold_v<KW, 4, 2, true>, 4, 4);
+        tv("tv W4 B2 noPF 2/CU", k_tab_fold_v<KW, 4, 2, false>, 4, 2);
+        tv("tv W4 B1 PF 4/CU", k_tab_fold_v<KW, 4, 1, true>, 4, 4);
+        tv("tv W4 B1 noPF 4/CU", k_tab_fold_v<KW, 4, 1, false>, 4, 4);
+        tv("tv W8 B2 PF 1/CU", k_tab_fold_v<KW, 8, 2, true>, 8, 1);
+        tv("tv W8 B2 PF 2/CU", k_tab_fold_v<KW, 8, 2, true>, 8, 2);
+        tv("tv W8 B2 noPF 2/CU", k_tab_fold_v<KW, 8, 2, false>, 8, 2);
+        tv("tv W8 B1 noPF 2/CU", k_tab_fold_v<KW, 8, 1, false>, 8, 2);
+        tv("tv W16 B2 noPF 1/CU", k_tab_fold_v<KW, 16, 2, false>, 16, 1);
+        tv("tv W16 B2 PF 1/CU", k_tab_fold_v<KW, 16, 2, true>, 16, 1);
         CK(hipFree(T));
     }
     std::vector<double> o1(m * L), o2(m * L);
