@@ -278,17 +278,21 @@ def tableau_block(spx, torch, m, n, args, device):
     every 63 pivots by an fp64-MFMA rank-63 update, so a pivot reads neither
     A nor B_w; the passes run in the persistent loop kernel (k_tab_loop).  Not
     the north-star loop (no per-pivot A / B^-1 stream): reported beside it.
-    Timed like the headline (W warmup pivots, then K), plus an event-timed run
-    for the loop / fold split and the fold kernel's roofline."""
+    Timed like the headline (W warmup pivots, then K rounded up to whole
+    windows of KW - 1 pivots, so the timed run holds exactly K / (KW - 1) folds
+    — at C5 the fold is most of a pivot's cost and a partial window would
+    under-count it), plus an event-timed run for the loop / fold split and the
+    fold kernel's roofline."""
     def run(timing):
         with spx.Context(m=m, n=n, seed=args.seed, device=device, timing=timing, tableau=True) as ctx:
             cfg = ctx.config()
+            per = max(cfg["window"] - 1, 1)
+            steps = per * max(1, -(-args.steps // per))
             ctx.iterate(args.warmup)
-            lt0 = ctx.loop_times() if timing else None
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             _, p0 = ctx.iterate(0)
-            _, p1 = ctx.iterate(args.steps)
+            _, p1 = ctx.iterate(steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             lt = ctx.loop_times() if timing else None

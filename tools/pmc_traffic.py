@@ -12,7 +12,7 @@ import json
 import statistics
 
 
-KERNELS = ("k_price", "k_update", "k_fold")
+KERNELS = ("k_price", "k_update", "k_tab_fold", "k_fold")
 
 
 def per_kernel(path, counter):
@@ -42,7 +42,7 @@ def main():
     out = {"m": a.m, "n": a.n, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes)",
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream half count), KiB -> bytes"}
     for k in KERNELS:
-        skip = a.skip if k != "k_fold" else 0  # a fold runs once per window
+        skip = a.skip if "fold" not in k else 0  # a fold runs once per window
         fv = f.get(k, [])[skip:]
         wv = w.get(k, [])[skip:]
         if not fv or not wv:
@@ -51,6 +51,9 @@ def main():
         wr = 1024.0 * statistics.median(wv)
         out[k] = {"launches": len(fv), "read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                   "raw_fetch_kib_median": statistics.median(fv), "raw_write_kib_median": statistics.median(wv)}
+        if "fold" in k:  # 8-byte-per-lane tile loads: the x2 stream correction may not hold
+            out[k]["note"] = "8 B/lane loads: read_bytes assumes the x2 correction; raw x1 = %.0f" % (
+                1024.0 * statistics.median(fv))
     if "k_price" in out:
         out["price_hbm_bytes_per_launch"] = out["k_price"]["hbm_bytes"]
     if "k_update" in out:
