@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void k_tab_fold_valu(TPar P, int nf, int cpw) 
 // Variants of the shipped tableau fold: WAVES waves per workgroup (16 columns
 // each, so 16 WAVES columns per workgroup), NBUF LDS buffers of staged U rows,
 // PF = next block's T tiles in flight during this block's MFMAs.
-template <int KW, int WAVES, int NBUF, bool PF>
+template <int KW, int WAVES, int NBUF, bool PF, int UP = TF_UP>
 __global__ __launch_bounds__(64 * WAVES) void k_tab_fold_v(TPar P, int min_nw) {
     constexpr int BLK = 64 * WAVES;
     const FakeSt* st = P.st;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_tab_fold_v(TPar P, int min_nw) {
     constexpr int KS = KW / 4;
     constexpr int KW2 = KW / 2;
     constexpr int UPT = TF_RB * KW2 / BLK;
-    __shared__ __attribute__((aligned(16))) double Ub[NBUF][TF_RB * TF_UP];
+    __shared__ __attribute__((aligned(16))) double Ub[NBUF][TF_RB * UP];
     const int ks = (nf + 3) / 4;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_tab_fold_v(TPar P, int min_nw) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
             const int pce = tid + BLK * k;
-            *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * TF_UP + 2 * (pce % KW2)]) = ur[k];
+            *reinterpret_cast<dbl2*>(&Ub[buf][(pce / KW2) * UP + 2 * (pce % KW2)]) = ur[k];
         }
     };
     auto tile_load = [&](int64_t i0, dbl4(&acc)[4]) {
@@ -579,7 +579,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_tab_fold_v(TPar P, int min_nw) {
             if (s < ks) {
 #pragma unroll
                 for (int it = 0; it < 4; ++it) {
-                    const double bv = ub[(16 * it + cl) * TF_UP + 4 * s + kr];
+                    const double bv = ub[(16 * it + cl) * UP + 4 * s + kr];
                     acc[it] = __builtin_amdgcn_mfma_f64_16x16x4f64(wf[s], bv, acc[it], 0, 0, 0);
                 }
             }
@@ -762,17 +762,47 @@ int main(int argc, char** argv) {
             if (gxv > maxx) gxv = maxx;
             tf(name, [&] { hipLaunchKernelGGL(kern, dim3(gxv, gyv), dim3(64 * waves), 0, 0, P, 2); });
         };
-        tv("tv W4 B2 PF (=shipped) 2/CU", k_tab_fold_v<KW, 4, 2, true>, 4, 2);
-        tv("tv W4 B2 PF 4/CU", k_tab_fold_v<KW, 4, 2, true>, 4, 4);
-        tv("tv W4 B2 noPF 2/CU", k_tab_fold_v<KW, 4, 2, false>, 4, 2);
-        tv("tv W4 B1 PF 4/CU", k_tab_fold_v<KW, 4, 1, true>, 4, 4);
-        tv("tv W4 B1 noPF 4/CU", k_tab_fold_v<KW, 4, 1, false>, 4, 4);
-        tv("tv W8 B2 PF 1/CU", k_tab_fold_v<KW, 8, 2, true>, 8, 1);
-        tv("tv W8 B2 PF 2/CU", k_tab_fold_v<KW, 8, 2, true>, 8, 2);
-        tv("tv W8 B2 noPF 2/CU", k_tab_fold_v<KW, 8, 2, false>, 8, 2);
-        tv("tv W8 B1 noPF 2/CU", k_tab_fold_v<KW, 8, 1, false>, 8, 2);
-        tv("tv W16 B2 noPF 1/CU", k_tab_fold_v<KW, 16, 2, false>, 16, 1);
-        tv("tv W16 B2 PF 1/CU", k_tab_fold_v<KW, 16, 2, true>, 16, 1);
+        tv("tv W8 B2 noPF 2/CU UP68 (=shipped)", k_tab_fold_v<KW, 8, 2, false, 68>, 8, 2);
+        tv("tv W8 B2 noPF 2/CU UP66", k_tab_fold_v<KW, 8, 2, false, 66>, 8, 2);
+        tv("tv W8 B2 noPF 2/CU UP70", k_tab_fold_v<KW, 8, 2, false, 70>, 8, 2);
+        tv("tv W8 B2 PF 2/CU UP66", k_tab_fold_v<KW, 8, 2, true, 66>, 8, 2);
+        tv("tv W4 B2 noPF 4/CU UP66", k_tab_fold_v<KW, 4, 2, false, 66>, 4, 4);
+        // the two folds of a tableau window: one after the other, or side by
+        // side on two streams (they share no written data once the window reset
+        // is left to a later kernel)
+        {
+            hipStream_t s1, s2;
+            CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+            CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            hipEvent_t ef, ej1, ej2;
+            CK(hipEventCreateWithFlags(&ef, hipEventDisableTiming));
+            CK(hipEventCreateWithFlags(&ej1, hipEventDisableTiming));
+            CK(hipEventCreateWithFlags(&ej2, hipEventDisableTiming));
+            auto tabl = [&](hipStream_t st, int per_cu) {
+                const long gyv = (n + 127) / 128;
+                long gxv = ((long)per_cu * 256 + gyv - 1) / gyv;
+                hipLaunchKernelGGL((k_tab_fold_v<KW, 8, 2, false, 68>), dim3(gxv, gyv), dim3(512), 0, st, P, 2);
+            };
+            auto foldl = [&](hipStream_t st, int ny) {
+                hipLaunchKernelGGL((k5_ship<true, true>), dim3(nx, ny), dim3(256), 0, st, B, U, Q, N, nf, m, L, sink);
+            };
+            tf("pair sequential (tab 2/CU, fold ny=8)", [&] { tabl(0, 2); foldl(0, 8); });
+            auto conc = [&](int tpc, int ny) {
+                CK(hipEventRecord(ef, 0));
+                CK(hipStreamWaitEvent(s1, ef, 0));
+                CK(hipStreamWaitEvent(s2, ef, 0));
+                foldl(s2, ny);
+                tabl(s1, tpc);
+                CK(hipEventRecord(ej1, s1));
+                CK(hipEventRecord(ej2, s2));
+                CK(hipStreamWaitEvent(0, ej1, 0));
+                CK(hipStreamWaitEvent(0, ej2, 0));
+            };
+            tf("pair concurrent (tab 2/CU, fold ny=8)", [&] { conc(2, 8); });
+            tf("pair concurrent (tab 1/CU, fold ny=4)", [&] { conc(1, 4); });
+            tf("pair concurrent (tab 2/CU, fold ny=4)", [&] { conc(2, 4); });
+            tf("pair concurrent (tab 4/CU, fold ny=8)", [&] { conc(4, 8); });
+        }
         CK(hipFree(T));
     }
     std::vector<double> o1(m * L), o2(m * L);
