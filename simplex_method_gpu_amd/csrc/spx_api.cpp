@@ -336,6 +336,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (P.tab) {
         SPX_TRY(x->alloc(&P.T, (size_t)(L * n)));
         SPX_TRY(x->alloc(&P.dw, (size_t)n));
+        SPX_TRY(x->alloc(&P.tab_list, (size_t)n));
+        SPX_TRY(x->alloc(&P.tab_cnt, (size_t)1));
     }
     P.pr_stride = P.win ? 1 + P.win / 2 : 1;
 

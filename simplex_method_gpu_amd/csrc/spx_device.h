@@ -208,6 +208,11 @@ struct Params {
     int32_t pad_t;
     double* T;
     double* dw;
+    // the fold's active columns (k_tab_active): those whose Wt row has a
+    // nonzero entry among the nf folded pivots; for every other column the
+    // fold adds U 0 = 0, so k_tab_fold walks this list instead of all n
+    int32_t* tab_list;  // n
+    int32_t* tab_cnt;   // 1
 };
 
 // Optimality test on the merged entering candidate (v4:299-302): the reduced

@@ -28,8 +28,42 @@ namespace spx {
 namespace {
 
 // ---------------------------------------------------------------------------
-// T_w += U Wt^T, dw += SY Wt^T.  A workgroup (TF_WAVES waves) owns 16
-// TF_WAVES columns of T_w and a range of rows, walked 64 rows at a time.  Wave
+// Active columns of a fold: j with Wt[j][t] != 0 for some t < nf (non-basic
+// columns, and basic ones that entered during the window).  A column basic
+// through the whole window has an all-zero Wt row (k_update writes the exact
+// entries of basic columns), so folding it adds U 0 = 0: skipping it changes
+// nothing (but the sign of an exact zero).  One thread per column; a wave
+// appends its active columns with one atomic (the list order does not matter:
+// each column's fold is independent of which wave does it).  P.tab_cnt is
+// zeroed by the launcher.
+// ---------------------------------------------------------------------------
+template <int KW>
+__global__ __launch_bounds__(256) void k_tab_active(Params P, int min_nw) {
+    const int nw = P.st->nw;
+    if (nw < min_nw || nw < 2) return;
+    const int nf = nw - 1;
+    const int lane = threadIdx.x & 63;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool act = false;
+    if (j < P.n) {
+        const dbl2* w = reinterpret_cast<const dbl2*>(P.Wt + j * KW);
+#pragma unroll
+        for (int k = 0; k < KW / 2; ++k) {
+            const dbl2 v = w[k];
+            act |= (2 * k < nf && v.x != 0.0) || (2 * k + 1 < nf && v.y != 0.0);  // NaN counts as nonzero
+        }
+    }
+    const unsigned long long b = __ballot(act);
+    int base = 0;
+    if (lane == 0 && b) base = atomicAdd(P.tab_cnt, (int)__popcll(b));
+    base = __shfl(base, 0, 64);
+    if (act) P.tab_list[base + __popcll(b & ((1ull << lane) - 1ull))] = (int32_t)j;
+}
+
+// T_w += U Wt^T, dw += SY Wt^T over the active columns (k_tab_active).  A
+// task is 16 TF_WAVES consecutive slots of the active list (their columns of
+// T_w) by a 64-row block; a workgroup (TF_WAVES waves) walks an equal,
+// contiguous range of tasks.  Wave
 // w keeps the Wt fragments of its 16 columns in registers (MFMA A operand,
 // lane: Wt[j0 + cl][4 s + kr]).  The eta rows U[i0 .. i0+64) of a block — 32
 // KiB, contiguous — are staged once per workgroup into LDS with 16-byte loads
@@ -48,7 +82,7 @@ constexpr int TF_RB = 64;  // rows per block
 constexpr int TF_UP = 68;  // LDS pitch of a staged eta row (doubles): 16-B aligned, spreads banks
 
 template <int KW>
-__global__ __launch_bounds__(TF_BLOCK) void k_tab_fold(Params P, int min_nw) {
+__global__ __launch_bounds__(TF_BLOCK, 4) void k_tab_fold(Params P, int min_nw) {  // 4 waves per SIMD: 2 workgroups per CU
     const DevState* st = P.st;
     const int nw = st->nw;
     if (nw < min_nw || nw < 2) return;
@@ -62,40 +96,50 @@ __global__ __launch_bounds__(TF_BLOCK) void k_tab_fold(Params P, int min_nw) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int cl = lane & 15, kr = lane >> 4;
-    const int64_t m = P.m, n = P.n, L = P.L;
+    const int64_t m = P.m, L = P.L;
     const double* __restrict__ U = P.U;
     const double* __restrict__ Wt = P.Wt;
     double* __restrict__ T = P.T;
-    const int64_t cb = (int64_t)blockIdx.y * 16 * TF_WAVES;  // this workgroup's columns
-
-    if (blockIdx.x == 0 && tid < 16 * TF_WAVES && cb + tid < n) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t]
-        const int64_t j = cb + tid;
-        double d = 0.0;
-        for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
-        P.dw[j] += d;
-    }
-    const int64_t per = ((m + gridDim.x - 1) / gridDim.x + TF_RB - 1) / TF_RB * TF_RB;
-    const int64_t i_lo = (int64_t)blockIdx.x * per;
-    const int64_t i_hi = (i_lo + per < m) ? i_lo + per : m;
-    if (cb >= n || i_lo >= i_hi) return;  // uniform per workgroup
-    const int64_t j0 = cb + 16 * wave;
+    const int cnt = *P.tab_cnt;  // active columns (k_tab_active)
+    const int32_t* __restrict__ lst = P.tab_list;
+    // tasks: (group of 16 TF_WAVES list slots, 64-row block), group-major; a
+    // workgroup takes a contiguous range, so every workgroup has the same
+    // amount of work whatever the active count (a grid over all n columns with
+    // early exits left a half-empty second round of workgroups)
+    const int64_t nblk = (m + TF_RB - 1) / TF_RB;
+    const int64_t ngrp = (cnt + 16 * TF_WAVES - 1) / (16 * TF_WAVES);
+    const int64_t K = ngrp * nblk;
+    const int64_t k_lo = K * blockIdx.x / gridDim.x, k_hi = K * (blockIdx.x + 1) / gridDim.x;
+    if (k_lo >= k_hi) return;  // uniform per workgroup
 
     double wf[KS];
+    int32_t jc[4];  // the columns of this lane's accumulator entries (slot s0 + kr + 4 r), -1: none
+    auto set_group = [&](int64_t g) {
+        const int s0 = (int)g * 16 * TF_WAVES + 16 * wave;  // this wave's 16 slots
+        const int64_t jw = (s0 + cl < cnt) ? (int64_t)lst[s0 + cl] : -1;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const int t = 4 * s + kr;
-        wf[s] = (j0 + cl < n && t < nf) ? Wt[(j0 + cl) * KW + t] : 0.0;
-    }
-    bool jok[4];
+        for (int s = 0; s < KS; ++s) {
+            const int t = 4 * s + kr;
+            wf[s] = (jw >= 0 && t < nf) ? Wt[jw * KW + t] : 0.0;
+        }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) jok[r] = j0 + kr + 4 * r < n;
-
+        for (int r = 0; r < 4; ++r) jc[r] = (s0 + kr + 4 * r < cnt) ? lst[s0 + kr + 4 * r] : -1;
+    };
+    auto dw_group = [&](int64_t g) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t], once per group
+        const int sl = (int)g * 16 * TF_WAVES + tid;
+        if (tid < 16 * TF_WAVES && sl < cnt) {
+            const int64_t j = lst[sl];
+            double d = 0.0;
+            for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
+            P.dw[j] += d;
+        }
+    };
     auto stage_load = [&](int64_t i0, dbl2 (&ur)[UPT]) {
 #pragma unroll
         for (int k = 0; k < UPT; ++k) {
             const int pce = tid + TF_BLOCK * k;
             const int64_t i = i0 + pce / KW2;
-            ur[k] = (pce < NST && i < i_hi) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
+            ur[k] = (pce < NST && i < m) ? reinterpret_cast<const dbl2*>(U)[i0 * KW2 + pce] : dbl2{0.0, 0.0};
         }
     };
     auto stage_write = [&](int buf, const dbl2 (&ur)[UPT]) {
@@ -110,21 +154,29 @@ __global__ __launch_bounds__(TF_BLOCK) void k_tab_fold(Params P, int min_nw) {
         for (int it = 0; it < 4; ++it) {
             const int64_t i = i0 + 16 * it + cl;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                acc[it][r] = (jok[r] && i < i_hi) ? T[(j0 + kr + 4 * r) * L + i] : 0.0;
+            for (int r = 0; r < 4; ++r) acc[it][r] = (jc[r] >= 0 && i < m) ? T[(int64_t)jc[r] * L + i] : 0.0;
         }
     };
 
+    int64_t g = k_lo / nblk, blk = k_lo % nblk;
+    set_group(g);
+    if (blk == 0) dw_group(g);
     dbl2 ur[UPT];
     dbl4 acc[4];
-    stage_load(i_lo, ur);
-    tile_load(i_lo, acc);
+    stage_load(blk * TF_RB, ur);
+    tile_load(blk * TF_RB, acc);
     stage_write(0, ur);
     __syncthreads();
     int buf = 0;
-    for (int64_t i0 = i_lo; i0 < i_hi; i0 += TF_RB, buf ^= 1) {
-        const bool more = i0 + TF_RB < i_hi;
-        if (more) stage_load(i0 + TF_RB, ur);
+    for (int64_t k = k_lo; k < k_hi; ++k, buf ^= 1) {
+        const int64_t i0 = blk * TF_RB;
+        const bool more = k + 1 < k_hi;
+        int64_t gn = g, bn = blk + 1;
+        if (bn == nblk) {
+            bn = 0;
+            gn = g + 1;
+        }
+        if (more) stage_load(bn * TF_RB, ur);
         const double* ub = Ub[buf];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
@@ -139,16 +191,22 @@ __global__ __launch_bounds__(TF_BLOCK) void k_tab_fold(Params P, int min_nw) {
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int64_t i = i0 + 16 * it + cl;
-            if (i < i_hi) {
+            if (i < m) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    if (jok[r]) T[(j0 + kr + 4 * r) * L + i] = acc[it][r];
+                    if (jc[r] >= 0) T[(int64_t)jc[r] * L + i] = acc[it][r];
             }
         }
         if (more) {
             stage_write(buf ^ 1, ur);
-            tile_load(i0 + TF_RB, acc);
+            if (gn != g) {  // next group: its Wt fragments and columns (bn == 0)
+                set_group(gn);
+                dw_group(gn);
+            }
+            tile_load(bn * TF_RB, acc);
         }
+        g = gn;
+        blk = bn;
         __syncthreads();
     }
 }
@@ -907,13 +965,19 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
 
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     if (!P.tab) return hipSuccess;
-    const int64_t gy = (P.n + 16 * TF_WAVES - 1) / (16 * TF_WAVES);
-    // rows split so that the grid has about 2 workgroups per CU (LDS: 68 KiB each)
-    int64_t gx = (2 * (int64_t)cus + gy - 1) / gy;
-    const int64_t maxx = (P.m + TF_RB - 1) / TF_RB;
-    if (gx > maxx) gx = maxx;
-    if (gx < 1) gx = 1;
-    const dim3 grid((unsigned)gx, (unsigned)gy);
+    hipError_t e = hipMemsetAsync(P.tab_cnt, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    const unsigned ga = (unsigned)((P.n + 255) / 256);
+    switch (P.win) {
+        case 8: hipLaunchKernelGGL(k_tab_active<8>, dim3(ga), dim3(256), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_tab_active<16>, dim3(ga), dim3(256), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_tab_active<32>, dim3(ga), dim3(256), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_tab_active<64>, dim3(ga), dim3(256), 0, s, P, min_nw); break;
+        default: return hipErrorInvalidValue;
+    }
+    // 2 workgroups per CU (LDS: 68 KiB each), all resident; each takes an equal
+    // share of the (column group, row block) tasks of the active list
+    const dim3 grid((unsigned)(2 * (cus > 0 ? cus : 1)));
     switch (P.win) {
         case 8: hipLaunchKernelGGL(k_tab_fold<8>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
         case 16: hipLaunchKernelGGL(k_tab_fold<16>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
