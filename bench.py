@@ -295,11 +295,12 @@ def tableau_block(spx, torch, m, n, args, device):
             _, p1 = ctx.iterate(steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            lt = ctx.loop_times() if timing else None
+            lt = ctx.loop_times() if timing else None  # fold events (and the persistent loop's)
+            pt = ctx.pass_times() if timing else None  # two-kernel passes
             info = ctx.info()
-        return cfg, dt, p1 - p0, lt, info
+        return cfg, dt, p1 - p0, (lt, pt), info
     cfg, dt, piv, _, info = run(False)
-    _, dt_e, piv_e, lt, _ = run(True)
+    _, dt_e, piv_e, (lt, pt), _ = run(True)
     L = info["ld"]
     win = cfg["window"]
     # the tableau fold touches the active columns only (k_tab_active): the
@@ -319,10 +320,14 @@ def tableau_block(spx, torch, m, n, args, device):
                           f"{win - 1} pivots; persistent loop kernel k_tab_loop ({cfg['loop_grid']} workgroups)"
                           if cfg.get("persistent") else f"window tableau {win}, two-kernel passes",
         "persistent": cfg.get("persistent", 0),
-        "loop": {"us_per_pass": 1e3 * lt["loop_ms"] / max(lt["loop_passes"], 1),
-                 "phase_us": {"pricing_to_barrier1": lt["price_us"] / passes,
-                              "ftran_ratio_to_barrier2": lt["ftran_us"] / passes,
-                              "leaving_row_bookkeeping": lt["tail_us"] / max(passes - 1, 1)}},
+        "loop": ({"us_per_pass": 1e3 * lt["loop_ms"] / max(lt["loop_passes"], 1),
+                  "phase_us": {"pricing_to_barrier1": lt["price_us"] / passes,
+                               "ftran_ratio_to_barrier2": lt["ftran_us"] / passes,
+                               "leaving_row_bookkeeping": lt["tail_us"] / max(passes - 1, 1)}}
+                 if cfg.get("persistent") else
+                 {"kernels": "k_price WM 3 + k_tab_update",
+                  "price_us": 1e3 * pt["price_ms"] / max(pt["passes"], 1),
+                  "update_us": 1e3 * pt["update_ms"] / max(pt["passes"], 1)}),
         "fold": {"kernels": "k_tab_active + k_tab_fold + k_fold", "avg_ms": fold_ms,
                  "per_pivot_us": 1e3 * fold_ms / (win - 1), "active_columns": n_act,
                  "algorithmic_bytes": fold_bytes, "flops": fold_flops,

@@ -524,6 +524,21 @@ void advance_window(spx_ctx* x, bool folded) {
     if (x->P.win) x->nw = (folded ? 1 : x->nw) + 1;
 }
 
+// The next pair of fold events (timing): spx_loop_times' fold_ms / folds.
+int fold_events(spx_ctx* x, hipEvent_t* f0, hipEvent_t* f1) {
+    if (x->ev_fold.size() < 2 * (x->n_fold + 1)) {
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            x->ev_fold.push_back(e);
+        }
+    }
+    *f0 = x->ev_fold[2 * x->n_fold];
+    *f1 = x->ev_fold[2 * x->n_fold + 1];
+    ++x->n_fold;
+    return SPX_OK;
+}
+
 // One loop pass: pricing, (MINLOC exchange), fused update.
 int enqueue_pass(spx_ctx* x, bool timed) {
     hipEvent_t p0 = nullptr, p1 = nullptr, u0 = nullptr, u1 = nullptr;
@@ -555,7 +570,13 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         ++x->n_update;
     }
     const bool fold = fold_due(x);
-    if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+    if (fold) {
+        hipEvent_t f0 = nullptr, f1 = nullptr;
+        if (timed) SPX_TRY(fold_events(x, &f0, &f1));
+        if (f0) HIP_TRY(hipEventRecord(f0, x->stream));
+        HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+        if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
+    }
     advance_window(x, fold);
     Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
     Pp.defer_price = x->defer_ok ? 1 : 0;
@@ -679,16 +700,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
         if (fold) {
             hipEvent_t f0 = nullptr, f1 = nullptr;
             if (x->timing) {
-                if (x->ev_fold.size() < 2 * (x->n_fold + 1)) {
-                    for (int i = 0; i < 2; ++i) {
-                        hipEvent_t e;
-                        HIP_TRY(hipEventCreate(&e));
-                        x->ev_fold.push_back(e);
-                    }
-                }
-                f0 = x->ev_fold[2 * x->n_fold];
-                f1 = x->ev_fold[2 * x->n_fold + 1];
-                ++x->n_fold;
+                SPX_TRY(fold_events(x, &f0, &f1));
                 HIP_TRY(hipEventRecord(f0, x->stream));
             }
             HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
