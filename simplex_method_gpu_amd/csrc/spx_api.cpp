@@ -645,6 +645,7 @@ int flush(spx_ctx* x) {
     if (x->stepped_price) return fail(SPX_ERR_STATE, "state readback between spx_price and spx_pivot");
     if (x->P.win) {  // fold every complete pivot: the explicit form the readback kernels expect
         HIP_TRY(launch_fold(x->P, 2, x->cus, x->stream));
+        HIP_TRY(launch_tab_binv(x->P, x->stream));  // tableau without k_fold: B_w from T_w
         x->nw = std::min(x->nw, 1);
     }
     HIP_TRY(launch_flush(x->P, x->stream));
@@ -885,6 +886,21 @@ int reinvert_current(spx_ctx* x) {
     return SPX_OK;
 }
 
+// Window tableau without k_fold (Params::tab_slack): needs A[:, n-m:] = I
+// exactly (the slack basis the reference's init assumes, v4:272-275).
+// A == nullptr: generated [U | I].  SPX_TAB_BW=1 keeps B_w and k_fold.
+bool tab_slack_ok(const double* A, int64_t m, int64_t n) {
+    const char* env = std::getenv("SPX_TAB_BW");
+    if (env && env[0] == '1') return false;
+    if (!A) return true;
+    for (int64_t i = 0; i < m; ++i) {
+        const double* col = A + (n - m + i) * m;  // column-major m x n
+        for (int64_t r = 0; r < m; ++r)
+            if (col[r] != (r == i ? 1.0 : 0.0)) return false;
+    }
+    return true;
+}
+
 int create_tail(spx_ctx* x) {
     SPX_TRY(do_reset(x));
     if (!x->use_comm && !x->persist) SPX_TRY(build_graph(x));  // capture + upload now (off any timed path)
@@ -914,6 +930,7 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
         if (e == hipSuccess) e = hipMemcpy(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     }
+    if (rc == SPX_OK && x->P.tab) x->P.tab_slack = tab_slack_ok(A, m, n) ? 1 : 0;
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;
@@ -936,6 +953,7 @@ int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed, con
         hipError_t e = launch_generate(x->A, x->b, x->c, m, n, x->L, seed, x->stream);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "generate failed: %s", hipGetErrorString(e));
     }
+    if (rc == SPX_OK && x->P.tab) x->P.tab_slack = tab_slack_ok(nullptr, m, n) ? 1 : 0;  // [U | I] by construction
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;

@@ -205,7 +205,10 @@ struct Params {
     // pass reads T_w[q_tau, j], dw[j] and Wt[j][.] per column instead of A_j,
     // and FTRAN reads the column T_w[:, p] instead of streaming B_w
     int32_t tab;
-    int32_t pad_t;
+    // A[:, n-m:] = I (checked at create): then B_w is T_w's slack block
+    // (B_w e_i = T_w[:, n-m+i]), so the tableau folds T_w, dw, y_w and xw
+    // only and skips k_fold; readbacks rebuild B_w from T_w (k_tab_binv)
+    int32_t tab_slack;
     double* T;
     double* dw;
     // the fold's active columns (k_tab_active): those whose Wt row has a

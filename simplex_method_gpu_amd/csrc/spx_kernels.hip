@@ -1635,6 +1635,10 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     if (P.tab) {  // T_w and dw first: k_fold resets the window
         const hipError_t e = launch_tab_fold(P, min_nw, cus, s);
         if (e != hipSuccess) return e;
+        // A[:, n-m:] = I: B_w is T_w's slack block and the tableau fold has
+        // updated y_w and xw too (and reset the window); B_w itself is rebuilt
+        // from T_w only for readbacks (launch_tab_binv)
+        if (P.tab_slack) return hipSuccess;
     }
     const int nx = (int)(P.L / 64);
     const dim3 grid((unsigned)nx, (unsigned)fold_grid_y(P.m, nx, cus));

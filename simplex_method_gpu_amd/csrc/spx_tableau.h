@@ -12,6 +12,8 @@ namespace spx {
 // when nw >= min_nw (the same test as k_fold, which must run after it: k_fold
 // resets nw).  No-op unless P.tab.
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s);
+// B_w from T_w's slack block (P.tab_slack; before readbacks that read B_w)
+hipError_t launch_tab_binv(const Params& P, hipStream_t s);
 // T_w = B_w A (B_w = P.B0, row-major): after a reinversion or a warm start.
 hipError_t launch_tab_build(const Params& P, hipStream_t s);
 // Persistent tableau loop (k_tab_loop): whole passes in one cooperative

@@ -53,6 +53,16 @@ __global__ __launch_bounds__(256) void k_tab_active(Params P, int min_nw) {
             act |= (2 * k < nf && v.x != 0.0) || (2 * k + 1 < nf && v.y != 0.0);  // NaN counts as nonzero
         }
     }
+    // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf) (k_fold's
+    // formula, t ascending), here when k_fold is skipped (P.tab_slack)
+    if (P.tab_slack && j < P.m) {
+        const double* wb = P.Wt + P.n * KW;
+        double d = 0.0;
+#pragma unroll
+        for (int t = 0; t < KW; ++t)
+            if (t < nf) d = fma(P.U[j * KW + t], wb[t], d);
+        P.xw[j] += d;
+    }
     const unsigned long long b = __ballot(act);
     int base = 0;
     if (lane == 0 && b) base = atomicAdd(P.tab_cnt, (int)__popcll(b));
@@ -125,6 +135,8 @@ __global__ __launch_bounds__(TF_BLOCK, 4) void k_tab_fold(Params P, int min_nw) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) jc[r] = (s0 + kr + 4 * r < cnt) ? lst[s0 + kr + 4 * r] : -1;
     };
+    const int64_t ns = P.n - m;  // first slack column
+    double* __restrict__ yw = st->y_buf ? P.y1 : P.y0;
     auto dw_group = [&](int64_t g) {  // dw[j] += sum_{t<nf} SY[t] Wt[j][t], once per group
         const int sl = (int)g * 16 * TF_WAVES + tid;
         if (tid < 16 * TF_WAVES && sl < cnt) {
@@ -132,6 +144,10 @@ __global__ __launch_bounds__(TF_BLOCK, 4) void k_tab_fold(Params P, int min_nw) 
             double d = 0.0;
             for (int t = 0; t < nf; ++t) d = fma(P.SY[t], Wt[j * KW + t], d);
             P.dw[j] += d;
+            // y_w += SY R (k_fold's term) when k_fold is skipped: R[t][i] =
+            // r_t . e_i = Wt[ns + i][t] for slack column ns + i (an inactive
+            // slack's row is all zero: no change)
+            if (P.tab_slack && j >= ns) yw[j - ns] += d;
         }
     };
     auto stage_load = [&](int64_t i0, dbl2 (&ur)[UPT]) {
@@ -961,7 +977,42 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     if (wg0 && tid == 0) La.ls->passes = (int32_t)(it - it0);
 }
 
+// The window reset k_fold's last workgroup does (the pending pivot stays
+// pending as tau = 0), when k_fold is skipped.
+__global__ void k_tab_reset(Params P, int min_nw) {
+    DevState* st = P.st;
+    const int nw = st->nw;
+    if (nw < min_nw || nw < 2) return;
+    P.SY[0] = P.SY[nw - 1];
+    st->nw = 1;
+}
+
+// B_w from T_w's slack block for readbacks (P.tab_slack): B_w[r][i] =
+// T_w[r, ns + i], a 64 x 64 tile per workgroup transposed through LDS.
+__global__ __launch_bounds__(256) void k_tab_binv(Params P) {
+    __shared__ double tile[64][65];
+    const int64_t m = P.m, L = P.L, ns = P.n - P.m;
+    const int64_t r0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int k = ty; k < 64; k += 4) {  // column i0 + k of the block, rows r0 + tx
+        const int64_t i = i0 + k, r = r0 + tx;
+        tile[k][tx] = (i < m && r < m) ? P.T[(ns + i) * L + r] : 0.0;
+    }
+    __syncthreads();
+    for (int k = ty; k < 64; k += 4) {  // row r0 + k of B_w, columns i0 + tx
+        const int64_t r = r0 + k, i = i0 + tx;
+        if (r < m && i < m) P.B0[r * L + i] = tile[tx][k];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_tab_binv(const Params& P, hipStream_t s) {
+    if (!P.tab || !P.tab_slack) return hipSuccess;
+    const unsigned g = (unsigned)((P.m + 63) / 64);
+    hipLaunchKernelGGL(k_tab_binv, dim3(g, g), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
 
 hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     if (!P.tab) return hipSuccess;
@@ -985,6 +1036,7 @@ hipError_t launch_tab_fold(const Params& P, int min_nw, int cus, hipStream_t s) 
         case 64: hipLaunchKernelGGL(k_tab_fold<64>, grid, dim3(TF_BLOCK), 0, s, P, min_nw); break;
         default: return hipErrorInvalidValue;
     }
+    if (P.tab_slack) hipLaunchKernelGGL(k_tab_reset, dim3(1), dim3(1), 0, s, P, min_nw);  // k_fold is skipped
     return hipGetLastError();
 }
 
