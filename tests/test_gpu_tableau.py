@@ -240,3 +240,31 @@ def test_tableau_large_invariants(spx, oracle, m, n, k, window):
     assert _rel(s["binv"] @ b, s["x_b"]) < 1e-10
     assert abs(z - float(c[s["b_ixs"]] @ s["x_b"])) <= 1e-10 * abs(z)
     assert np.all(s["x_b"] > -1e-9)
+
+
+@pytest.mark.parametrize("keep_bw", ["0", "1"])
+def test_tableau_bw_forms_match_oracle(spx, oracle, monkeypatch, keep_bw):
+    """With A[:, n-m:] = I the tableau skips k_fold (B_w is T_w's slack block,
+    rebuilt for readbacks by k_tab_binv); SPX_TAB_BW=1 keeps B_w and k_fold.
+    Both follow the oracle across several folds (window 16, 150 pivots)."""
+    monkeypatch.setenv("SPX_TAB_BW", keep_bw)
+    m, n, k = 257, 771, 150
+    A, b, c = oracle.generate(m, n, 2)
+    ref = oracle.solve(A, b, c, max_iter=k, eps=1e-7, want_state=True, trace_cap=k)
+    with spx.Context(A, b, c, eps=1e-7, window=16, tableau=True, persist=False) as ctx:
+        st, piv = ctx.iterate(k)
+        s = ctx.state(binv=True)
+        z = ctx.objective()
+        # a readback mid-solve, then more pivots: the rebuilt B_w stays consistent
+        st2, piv2 = ctx.iterate(20)
+        s2 = ctx.state(binv=True)
+    assert piv == ref.pivots
+    assert list(s["b_ixs"]) == list(ref.b_ixs)
+    assert _rel(s["x_b"], ref.x_b) <= 1e-9
+    assert _rel(s["y"], ref.y) <= 1e-9
+    assert _rel(s["binv"], ref.binv) <= 1e-9
+    assert abs(z - ref.z) <= 1e-9 * abs(ref.z)
+    ref2 = oracle.solve(A, b, c, max_iter=k + piv2, eps=1e-7, want_state=True, trace_cap=k + piv2)
+    assert list(s2["b_ixs"]) == list(ref2.b_ixs)
+    assert _rel(s2["binv"], ref2.binv) <= 1e-9
+    assert _rel(s2["x_b"], ref2.x_b) <= 1e-9
