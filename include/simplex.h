@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 4
+#define SPX_ABI_VERSION 5
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -92,7 +92,13 @@ typedef struct spx_opts {
     int32_t pricing;      /* entering-column rule, SPX_PRICING_* (default DANTZIG) */
     int32_t loop_block;   /* tuning: threads per workgroup of the persistent loop
                              kernel (512 / 1024), 0 = auto                     */
-    int32_t reserved[2];
+    int32_t trace_cap;    /* record the first trace_cap pivots' (entering column
+                             p, leaving row q) on the device, written by the
+                             kernel that commits each pivot (spx_get_trace);
+                             0 = off.  The reference prints nothing of the
+                             kind; the parity tests compare it with the
+                             oracle's pivot sequence.                        */
+    int32_t reserved;
 } spx_opts;
 
 /* Entering-column rules (README.md:16-17 "steepest edge").
@@ -246,6 +252,12 @@ int spx_reduced_costs(spx_ctx* ctx, double* e);
 /* Objective z = c_B . x_b (v4:365), computed on the device. */
 int spx_objective(spx_ctx* ctx, double* z);
 
+/* Pivot trace (opts.trace_cap > 0): copies the first min(pivots made,
+ * trace_cap, cap) pivots' entering columns into p[] and leaving rows into q[]
+ * (either may be NULL) and stores that count in *count.  Indexed by pivot
+ * number, so a spx_reset / re-solve overwrites it. */
+int spx_get_trace(spx_ctx* ctx, int64_t* p, int64_t* q, int64_t cap, int64_t* count);
+
 /* With SPX_FLAG_TIMING: total device milliseconds and launch counts of the
  * pricing kernel and of the fused update kernel since the last call (resets). */
 int spx_kernel_times(spx_ctx* ctx, double* price_ms, int64_t* price_launches,
@@ -295,6 +307,17 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * (SPX_FLAG_TABLEAU) in use, [11] workgroups of the persistent loop kernel. */
 #define SPX_CONFIG_FIELDS 12
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
+
+/* What the loop has enqueued since spx_create (monotone counters, so a
+ * caller can difference them around a timed region): out[0] passes launched
+ * eagerly (step-wise spx_price/spx_pivot included), [1] captured-hipGraph
+ * replays, [2] passes inside those replays, [3] persistent loop-kernel
+ * launches, [4] passes inside them, [5] eta-window folds (k_fold) enqueued,
+ * [6] the window position (pivots since the last fold + 1; a fold is due
+ * before the next pass when it equals [7]), [7] the window size KW (0 =
+ * explicit B^-1). */
+#define SPX_DISPATCH_FIELDS 8
+int spx_dispatch_stats(spx_ctx* ctx, int64_t out[SPX_DISPATCH_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:
  * spx_shard_range: this rank's column shard — structural columns

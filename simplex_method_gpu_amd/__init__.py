@@ -131,7 +131,7 @@ class Context:
                  global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
                  ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0,
                  pricing: int = 0, persist: bool | None = None, loop_block: int = 0, comm1: bool = False,
-                 tableau: bool = False):
+                 tableau: bool = False, trace: int = 0):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -143,6 +143,7 @@ class Context:
         o.refactor_every = refactor_every
         o.pricing = pricing  # PRICING_DANTZIG / PRICING_DEVEX
         o.loop_block = loop_block
+        o.trace_cap = trace  # record the first `trace` pivots' (p, q) on the device
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
                    | (FLAG_SPLIT_TAIL if split_tail else 0)
@@ -216,6 +217,19 @@ class Context:
                                 ctypes.byref(st), ctypes.byref(piv)))
         return SolveResult(z.value, SolveStatus(st.value), x_b, b_ixs, piv.value)
 
+    def trace(self):
+        """(entering columns, leaving rows) of the pivots recorded so far
+        (needs ``trace=K`` at construction; spx_get_trace)."""
+        cap = self.pivots_made()
+        p = np.zeros(max(cap, 1), dtype=np.int64)
+        q = np.zeros(max(cap, 1), dtype=np.int64)
+        k = ctypes.c_int64()
+        check(self._L.spx_get_trace(self._h, _ptr(p), _ptr(q), cap, ctypes.byref(k)))
+        return p[:k.value], q[:k.value]
+
+    def pivots_made(self) -> int:
+        return self.iterate(0)[1]
+
     def price(self):
         p, e, opt = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int32()
         check(self._L.spx_price(self._h, ctypes.byref(p), ctypes.byref(e), ctypes.byref(opt)))
@@ -288,6 +302,14 @@ class Context:
         return {"m": m.value, "n": n.value, "ld": ld.value, "local_nonbasic": nb.value,
                 "bytes_price": bp.value, "bytes_update": bu.value}
 
+
+    def dispatch_stats(self):
+        """Monotone counts of what the loop enqueued (spx_dispatch_stats)."""
+        out = (ctypes.c_int64 * 8)()
+        check(self._L.spx_dispatch_stats(self._h, out))
+        keys = ("eager_passes", "graph_launches", "graph_passes", "persistent_launches", "persistent_passes",
+                "folds", "window_pos", "window")
+        return dict(zip(keys, list(out)))
 
     def config(self):
         """Resolved representation and launch geometry (spx_config)."""

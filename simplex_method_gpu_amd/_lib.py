@@ -37,7 +37,8 @@ class SpxOpts(ctypes.Structure):
         ("feas_tol", ctypes.c_double),
         ("pricing", ctypes.c_int32),
         ("loop_block", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 2),
+        ("trace_cap", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -57,6 +58,8 @@ SIGNATURES = {
     "spx_iterate": (ctypes.c_int, [_p, _i64, _p, _p]),
     "spx_price": (ctypes.c_int, [_p, _p, _p, _p]),
     "spx_pivot": (ctypes.c_int, [_p, _p, _p]),
+    "spx_dispatch_stats": (ctypes.c_int, [_p, _p]),
+    "spx_get_trace": (ctypes.c_int, [_p, _p, _p, _i64, _p]),
     "spx_get_state": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p]),
     "spx_reduced_costs": (ctypes.c_int, [_p, _p]),
     "spx_objective": (ctypes.c_int, [_p, _p]),

@@ -128,6 +128,11 @@ struct spx_ctx {
     int32_t status = SPX_STATUS_MAX_ITER;
     bool stepped_price = false;
     int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
+    // what the loop actually enqueued (spx_dispatch_stats)
+    int64_t n_eager = 0, n_graph_launch = 0, n_graph_pass = 0, n_persist_launch = 0, n_persist_pass = 0;
+    int64_t n_folds = 0;
+    int graph_folds = 0;     // folds inside one captured batch
+    bool capturing = false;  // build_graph: passes are recorded, not run
 
     // persistent loop kernel (spx_loop.h): window mode, one rank
     LoopCfg lcfg{};
@@ -290,6 +295,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.nb_list, (size_t)n));
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
     SPX_TRY(x->alloc(&P.st, 1));
+    if (x->opts.trace_cap < 0) return fail(SPX_ERR_ARG, "trace_cap must be >= 0");
+    if (x->opts.trace_cap > 0) {
+        P.trace_cap = x->opts.trace_cap;
+        SPX_TRY(x->alloc(&P.trace, (size_t)(2 * P.trace_cap)));
+    }
 
     // B^-1 representation: eta window of KW pivots, or the explicit rank-1 update
     int KW = x->opts.window;
@@ -570,6 +580,11 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         ++x->n_update;
     }
     const bool fold = fold_due(x);
+    if (x->capturing) x->graph_folds += fold ? 1 : 0;
+    else {
+        ++x->n_eager;
+        x->n_folds += fold ? 1 : 0;
+    }
     if (fold) {
         hipEvent_t f0 = nullptr, f1 = nullptr;
         if (timed) SPX_TRY(fold_events(x, &f0, &f1));
@@ -603,7 +618,10 @@ int build_graph(spx_ctx* x) {
     int rc = SPX_OK;
     const int nw_keep = x->nw;
     if (x->P.win) x->nw = x->P.win;  // a batch starts with a fold (see iterate)
+    x->capturing = true;
+    x->graph_folds = 0;
     for (int i = 0; i < x->batch && rc == SPX_OK; ++i) rc = enqueue_pass(x, false);
+    x->capturing = false;
     x->nw = nw_keep;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(x->stream, &g);
@@ -707,6 +725,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
             HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
             if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
             x->nw = 1;
+            ++x->n_folds;
         }
         const int64_t np = std::min<int64_t>(left, x->P.win - x->nw);
         LoopArgs a = x->la;
@@ -731,6 +750,8 @@ int iterate_persist(spx_ctx* x, int64_t k) {
             HIP_TRY(hipEventRecord(e0, x->stream));
         }
         HIP_TRY(x->P.tab ? launch_tab_loop(x->P, a, x->lcfg, x->stream) : launch_loop(x->P, a, x->lcfg, x->stream));
+        ++x->n_persist_launch;
+        x->n_persist_pass += np;
         if (e1) HIP_TRY(hipEventRecord(e1, x->stream));
         if (x->timing) {  // phase split from workgroup 0's clock (s_memrealtime, 100 MHz)
             unsigned long long ck[3 * 64];
@@ -776,6 +797,9 @@ int iterate_raw(spx_ctx* x, int64_t k) {
             SPX_TRY(build_graph(x));
             const int64_t reps = left / x->batch;
             for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
+            x->n_graph_launch += reps;
+            x->n_graph_pass += reps * x->batch;
+            x->n_folds += reps * x->graph_folds;
             left -= reps * x->batch;  // a batch of whole windows leaves nw == KW again
         }
     }
@@ -1098,6 +1122,8 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 const bool fold = fold_due(x);
                 if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
                 advance_window(x, fold);
+                ++x->n_eager;
+                x->n_folds += fold ? 1 : 0;
                 HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
                 HIP_TRY(hipEventRecord(x->ev_sent, x->stream));
             }
@@ -1186,6 +1212,22 @@ int spx_objective(spx_ctx* x, double* z) {
     return SPX_OK;
 }
 
+int spx_get_trace(spx_ctx* x, int64_t* p, int64_t* q, int64_t cap, int64_t* count) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (cap < 0) return fail(SPX_ERR_ARG, "cap must be >= 0");
+    if (!x->P.trace) return fail(SPX_ERR_STATE, "no pivot trace: create the context with opts.trace_cap > 0");
+    SPX_TRY(read_state(x));
+    const int64_t k = std::min(std::min<int64_t>(x->pivots, x->P.trace_cap), cap);
+    std::vector<int64_t> buf((size_t)(2 * std::max<int64_t>(k, 1)));
+    if (k > 0) HIP_TRY(hipMemcpy(buf.data(), x->P.trace, sizeof(int64_t) * 2 * (size_t)k, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < k; ++i) {
+        if (p) p[i] = buf[2 * i];
+        if (q) q[i] = buf[2 * i + 1];
+    }
+    if (count) *count = k;
+    return SPX_OK;
+}
+
 int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_b, double* binv, int32_t* status,
                   int64_t* pivots) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
@@ -1259,6 +1301,8 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     SPX_TRY(set_limit(x, x->pivots + 1));
     const bool fold = fold_due(x);
     if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
+    ++x->n_eager;
+    x->n_folds += fold ? 1 : 0;
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
     const int ps = x->P.pr_stride;
     if (x->use_comm) {
@@ -1291,6 +1335,19 @@ int spx_pivot(spx_ctx* x, int64_t* q, int32_t* status) {
     SPX_TRY(read_state(x));
     if (q) *q = (x->status == SPX_STATUS_UNBOUNDED) ? -1 : x->st_host->q;
     if (status) *status = x->status;
+    return SPX_OK;
+}
+
+int spx_dispatch_stats(spx_ctx* x, int64_t out[SPX_DISPATCH_FIELDS]) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    out[0] = x->n_eager;
+    out[1] = x->n_graph_launch;
+    out[2] = x->n_graph_pass;
+    out[3] = x->n_persist_launch;
+    out[4] = x->n_persist_pass;
+    out[5] = x->n_folds;
+    out[6] = x->P.win ? x->nw : 0;
+    out[7] = x->P.win;
     return SPX_OK;
 }
 

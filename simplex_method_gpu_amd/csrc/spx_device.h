@@ -216,7 +216,18 @@ struct Params {
     // fold adds U 0 = 0, so k_tab_fold walks this list instead of all n
     int32_t* tab_list;  // n
     int32_t* tab_cnt;   // 1
+    // pivot trace (spx_opts.trace_cap): trace[2 it] = p, trace[2 it + 1] = q
+    // for pivot it < trace_cap, written where the pivot is committed
+    int64_t* trace;
+    int64_t trace_cap;
 };
+
+__device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {
+    if (P.trace && it < P.trace_cap) {
+        P.trace[2 * it] = p;
+        P.trace[2 * it + 1] = q;
+    }
+}
 
 // Optimality test on the merged entering candidate (v4:299-302): the reduced
 // cost itself under Dantzig; under Devex the key -e^2/w is +inf exactly when

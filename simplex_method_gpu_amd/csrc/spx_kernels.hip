@@ -593,6 +593,7 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
     st->q = q;
     st->min_e = min_e;  // the entering reduced cost (callers resolve Devex's key)
     st->iter = it + 1;
+    record_pivot(P, it, p, q);
 }
 
 // The last workgroup of k_update (single rank / replicated B^-1): leaving

@@ -521,6 +521,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
             st->q = qn;
             st->min_e = P.devex ? S.pwin.pad : min_e;
             st->iter = it + 1;
+            record_pivot(P, it, p, qn);
             if (P.devex) {
                 st->leave = leave;
                 st->wp = wp_new;
@@ -597,7 +598,11 @@ hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c) {
 hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s) {
     void* args[] = {const_cast<Params*>(&P), const_cast<LoopArgs*>(&a)};
     const void* fn = c.lds_r ? fn_t<512, true>() : fn_t<512, false>();
-    return hipLaunchCooperativeKernel(fn, dim3(c.grid), dim3(c.block), args, (unsigned)c.lds_bytes, s);
+    // a plain launch: the grid (one workgroup per CU, per_cu >= 1 checked in
+    // loop_prepare) is co-resident without the cooperative launch's check,
+    // and the grid barrier is our own (spx_grid.h), so no cooperative queue
+    // (MI355X_MICROARCH.md coop-launch: +15-19 us host wall per launch)
+    return hipLaunchKernel(fn, dim3(c.grid), dim3(c.block), args, (size_t)c.lds_bytes, s);
 }
 
 }  // namespace spx

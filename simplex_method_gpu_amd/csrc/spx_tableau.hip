@@ -575,6 +575,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
             st->q = bk_qn;
             st->min_e = bk_mine;
             st->iter = bk_it + 1;
+            record_pivot(P, bk_it, bk_p, bk_qn);
             if (P.devex) {
                 st->leave = bk_leave;
                 st->wp = bk_wp;
@@ -1108,8 +1109,10 @@ void tab_loop_partial_bytes(const LoopCfg& c, size_t* xp, size_t* xu) {
 hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s) {
     int cpw = c.cpw, rw = c.rw;
     void* args[] = {const_cast<Params*>(&P), const_cast<LoopArgs*>(&a), &cpw, &rw};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(c.grid),
-                                      dim3(c.block), args, (unsigned)c.lds_bytes, s);
+    // plain launch of a co-resident grid (c.grid <= CUs, per_cu >= 1): the
+    // barriers and hand-offs are our own, see launch_loop
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(c.grid), dim3(c.block), args,
+                           (size_t)c.lds_bytes, s);
 }
 
 }  // namespace spx

@@ -36,12 +36,12 @@ def test_opts_layout_matches_header(spx, tmp_path):
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "simplex.h"\n'
         "int main(void){printf(\"%zu %zu %zu %zu\\n\", sizeof(spx_opts), offsetof(spx_opts, device),"
-        " offsetof(spx_opts, flags), offsetof(spx_opts, reserved));return 0;}\n")
+        " offsetof(spx_opts, flags), offsetof(spx_opts, trace_cap));return 0;}\n")
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     S = spx._lib.SpxOpts
-    assert [int(v) for v in out] == [ctypes.sizeof(S), S.device.offset, S.flags.offset, S.reserved.offset]
+    assert [int(v) for v in out] == [ctypes.sizeof(S), S.device.offset, S.flags.offset, S.trace_cap.offset]
 
 
 def test_default_opts(spx):
@@ -54,7 +54,7 @@ def test_status_strings(spx):
     L = spx._lib.load()
     assert L.spx_status_string(0) == b"MAX_ITER exceeded."
     assert L.spx_status_string(2) == b"Problem unbounded."
-    assert L.spx_abi_version() == 4
+    assert L.spx_abi_version() == 5
 
 
 def _has_gpu():
