@@ -295,6 +295,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.nb_list, (size_t)n));
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
     SPX_TRY(x->alloc(&P.st, 1));
+    SPX_TRY(x->alloc(&P.arrive, (size_t)(ARR_GROUPS * ARR_LINES * ARR_STRIDE)));
     if (x->opts.trace_cap < 0) return fail(SPX_ERR_ARG, "trace_cap must be >= 0");
     if (x->opts.trace_cap > 0) {
         P.trace_cap = x->opts.trace_cap;
@@ -419,7 +420,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     }
 
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
-    SPX_TRY(x->alloc(&P.upd_partials, (size_t)uc.grid));
+    P.upd_cap = uc.grid;
+    SPX_TRY(x->alloc(&P.upd_soa, (size_t)(7 * uc.grid)));
     // the persistent loop kernel replaces the two-kernel pass where it applies
     if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {

@@ -107,6 +107,13 @@ struct alignas(16) RsHeader {
     int64_t pad;
 };
 
+// sharded last-arrival counters (arrive_last, spx_common.h): per group one
+// root line and ARR_SHARDS shard lines of 128 bytes
+constexpr int ARR_SHARDS = 8;
+constexpr int ARR_STRIDE = 32;  // uint32 per 128-byte line
+constexpr int ARR_LINES = 1 + ARR_SHARDS;
+enum : int { ARR_PRICE = 0, ARR_UPDATE = 1, ARR_FOLD = 2, ARR_GROUPS = 3 };
+
 struct alignas(16) DevState {
     int32_t status;      // ST_*
     int32_t nb_count;    // entries in nb_list
@@ -121,10 +128,10 @@ struct alignas(16) DevState {
     int64_t y_applied;   // ybuf[y_buf] includes the first y_applied pivots
     int64_t xb_applied;  // x_b includes the first xb_applied pivots
     int32_t y_buf;
-    uint32_t ticket_price;
-    uint32_t ticket_update;
+    uint32_t pad_t0;     // (the arrival counters live in Params::arrive)
+    uint32_t pad_t1;
     int32_t nw;          // eta window: pivots since the last fold (nw-1 pending)
-    uint32_t ticket_fold;
+    uint32_t pad_t2;
     int32_t pad1;
     int64_t leave;       // Devex: column that left at the last pivot (-1 none)
     double wp;           // Devex: weight of the last entering column
@@ -165,7 +172,8 @@ struct Params {
     int32_t nin;
     int32_t pr_stride;             // ArgMinEntry slots per record: 1, or 1 + KW/2
                                    // (the window appends Wt[p][0..KW) to the head)
-    UpdPartial* upd_partials;
+    double* upd_soa;               // k_update partials, field-major (upd_publish)
+    int64_t upd_cap;               // workgroup slots per field
     DevState* st;
     // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
     // global rows [r0, r0 + mloc) of B^-1, stored as B0/B1 (mloc x L ping-pong)
@@ -220,6 +228,9 @@ struct Params {
     // for pivot it < trace_cap, written where the pivot is committed
     int64_t* trace;
     int64_t trace_cap;
+    // sharded last-arrival counters (spx_common.h arrive_last), ARR_GROUPS
+    // groups of ARR_LINES 128-byte lines
+    uint32_t* arrive;
 };
 
 __device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {

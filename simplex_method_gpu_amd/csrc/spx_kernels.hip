@@ -20,7 +20,8 @@
 // Cross-workgroup hand-offs inside a launch (partials, alpha) use agent-scope
 // relaxed atomic stores/loads (global_* sc1: L1 bypass) drained with
 // s_waitcnt vmcnt(0) before a workgroup barrier and one agent-scope ticket
-// add per workgroup (MI355X_MICROARCH.md, Valid forms, first table row).
+// add per workgroup (MI355X_MICROARCH.md, Valid forms, first table row), on
+// sharded counters (arrive_last, spx_common.h).
 // Everything is deterministic: fixed reduction orders, no float atomics, so
 // results are bit-identical for any grid / block size and any shard count.
 #include <hip/hip_runtime.h>
@@ -414,9 +415,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             st_agent(&P.price_partials[blockIdx.x].pad, w.pad);
         }
         drain_vmem();
-        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_price, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = (t == gridDim.x - 1);
+        *s_last = arrive_last(arrive_group(P.arrive, ARR_PRICE), gridDim.x, blockIdx.x);
     }
     __syncthreads();
     if (!*s_last) return;
@@ -448,7 +447,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if (tid == 0) {
         P.price_out[0] = ArgMinEntry{t.val, t.idx};
         if (WIN && P.devex) *P.dvx_e = t.pad;
-        st_agent(&st->ticket_price, 0u);
     }
     if (WIN && P.nin > 1) {
         // the winner's window coefficients Wt[p][0..nw) travel with it (the
@@ -479,6 +477,37 @@ __device__ double block_sum(double a, double* sa) {
     return t;
 }
 
+// Ratio-test partials of the k_update workgroups, stored field-major: field f
+// of workgroup g at upd_soa[f * upd_cap + g].  A wave's loads of one field
+// over 64 workgroups are then 512 contiguous bytes; with 64-byte records every
+// lane's field load was a line of its own (7 x 512 line requests from the one
+// CU that runs the tail).
+__device__ __forceinline__ void upd_publish(const Params& P, int g, const UpdPartial& w) {
+    double* const s = P.upd_soa + g;
+    const int64_t c = P.upd_cap;
+    st_agent(&s[0 * c], w.theta);
+    st_agent(reinterpret_cast<int64_t*>(&s[1 * c]), w.idx);
+    st_agent(reinterpret_cast<int64_t*>(&s[2 * c]), w.nonpos);
+    st_agent(&s[3 * c], w.T);
+    st_agent(&s[4 * c], w.a_w);
+    st_agent(&s[5 * c], w.cb_w);
+    st_agent(reinterpret_cast<int64_t*>(&s[6 * c]), w.bix_w);
+}
+__device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g) {
+    const double* const s = P.upd_soa + g;
+    const int64_t c = P.upd_cap;
+    UpdPartial v;
+    v.theta = ld_agent(&s[0 * c]);
+    v.idx = ld_agent(reinterpret_cast<const int64_t*>(&s[1 * c]));
+    v.nonpos = ld_agent(reinterpret_cast<const int64_t*>(&s[2 * c]));
+    v.T = ld_agent(&s[3 * c]);
+    v.a_w = ld_agent(&s[4 * c]);
+    v.cb_w = ld_agent(&s[5 * c]);
+    v.bix_w = ld_agent(reinterpret_cast<const int64_t*>(&s[6 * c]));
+    v.pad = 0;
+    return v;
+}
+
 // Leaving argmin over the k_update workgroup partials + unbounded count
 // (v4:317-325), carrying the winner's scalars.  One dependent round trip
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
@@ -487,34 +516,37 @@ template <int BLOCK>
 __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    UpdPartial w = upd_empty();
-    for (int g = tid; g < nparts; g += BLOCK) {
-        const UpdPartial* src = &P.upd_partials[g];
-        UpdPartial v;
-        v.theta = ld_agent(&src->theta);
-        v.idx = ld_agent(&src->idx);
-        v.nonpos = ld_agent(&src->nonpos);
-        v.T = ld_agent(&src->T);
-        v.a_w = ld_agent(&src->a_w);
-        v.cb_w = ld_agent(&src->cb_w);
-        v.bix_w = ld_agent(&src->bix_w);
-        upd_merge(w, v);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        // butterfly partner merge in a fixed role order: lower lane's value first
-        const UpdPartial o = upd_shfl_xor(w, off);
-        UpdPartial lo = (lane & off) ? o : w;
-        const UpdPartial hi = (lane & off) ? w : o;
-        upd_merge(lo, hi);
-        w = lo;
-    }
-    if (lane == 0) red[wave] = w;
-    __syncthreads();
+    // every slot's seven fields are loaded before any is used (one round trip)
+    UpdPartial w = (tid < nparts) ? upd_fetch(P, tid) : upd_empty();
+    for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch(P, g));
+    // wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
+    // winner's scalars come from its lane by readlane
+    double th = w.theta;
+    int64_t ix = w.idx;
+    double T = w.T;
+    int np = (int)w.nonpos;
+    lane_argmin<64>(th, ix);
+    lane_sum<64>(T);
+    lane_isum<64>(np);
+    th = readlane_d(th, 63);
+    ix = readlane_l(ix, 63);
+    const uint64_t hit = __ballot(w.theta == th && w.idx == ix);
+    const int wl = hit ? (int)__builtin_ctzll(hit) : 0;
+    UpdPartial o;  // (cross-lane reads outside the lane-0 branch)
+    o.theta = th;
+    o.idx = ix;
+    o.nonpos = __builtin_amdgcn_readlane(np, 63);
+    o.T = readlane_d(T, 63);
+    o.a_w = readlane_d(w.a_w, wl);
+    o.cb_w = readlane_d(w.cb_w, wl);
+    o.bix_w = readlane_l(w.bix_w, wl);
+    o.pad = 0;
+    if (lane == 0) red[wave] = o;
+    lds_barrier();
     UpdPartial t = red[0];
 #pragma unroll
     for (int k = 1; k < WAVES; ++k) upd_merge(t, red[k]);
-    __syncthreads();
+    lds_barrier();
     return t;
 }
 
@@ -539,11 +571,13 @@ struct TailPre {
     double wp;  // Devex: the entering column's weight
     bool has_e;
     double e_enter;  // deferred pricing tail: the entering column's reduced cost
+    int32_t nw;      // eta window: pivots in the window (stable until the tail)
 };
 
 __device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState* st, int64_t p) {
-    TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
+    TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
     if (p < 0 || p >= P.n) return t;
+    if (P.win) t.nw = st->nw;
     t.c_p = P.c[p];
     t.cnt = st->nb_count;
     if (owns_col(P, p)) {
@@ -578,8 +612,9 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
     st->aq = aq;
     st->s_y = s_y;
     if (P.win) {  // eta window: the pivot joins the window as its pending entry
-        P.SY[st->nw] = s_y;
-        st->nw = st->nw + 1;
+        const int32_t nw = (pre && pre->valid) ? pre->nw : st->nw;
+        P.SY[nw] = s_y;
+        st->nw = nw + 1;
     } else {
         if (st->y_applied < it) st->y_buf ^= 1;  // k_price of this pass persisted y
         st->y_applied = it;
@@ -615,13 +650,11 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
         st->p = p;
         st->min_e = min_e;
         st->status = ST_UNBOUNDED;
-        st_agent(&st->ticket_update, 0u);
         return;
     }
     const double c_p = pre ? pre->c_p : P.c[p];
     const double e_rep = !P.devex ? min_e : (pre && pre->has_e ? pre->e_enter : *P.dvx_e);
     pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, c_p), e_rep, it, pre);
-    st_agent(&st->ticket_update, 0u);
     tail_mark(P, 1, tm);
 }
 
@@ -976,31 +1009,21 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         if (tid == 0) {
             UpdPartial w = red[0];
             for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
-            P.upd_partials[blockIdx.x] = w;
+            upd_publish(P, blockIdx.x, w);
         }
         return;
     }
     if (tid == 0) {
         UpdPartial w = red[0];
         for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
-        UpdPartial* dstp = &P.upd_partials[blockIdx.x];
-        st_agent(&dstp->theta, w.theta);
-        st_agent(&dstp->idx, w.idx);
-        st_agent(&dstp->nonpos, w.nonpos);
-        st_agent(&dstp->T, w.T);
-        st_agent(&dstp->a_w, w.a_w);
-        st_agent(&dstp->cb_w, w.cb_w);
-        st_agent(&dstp->bix_w, w.bix_w);
+        upd_publish(P, blockIdx.x, w);
         drain_vmem();  // the partial is visible before the ticket
-        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = (t == gridDim.x - 1);
+        *s_last = arrive_last(arrive_group(P.arrive, ARR_UPDATE), gridDim.x, blockIdx.x);
     }
     __syncthreads();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
 #ifdef SPX_DIAG_SKIP_TAIL  // timing-only build: pivots stop after the first pass
-    if (tid == 0) st_agent(&st->ticket_update, 0u);
     if (true) return;
 #endif
     if constexpr (RS)
@@ -1122,20 +1145,11 @@ __global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
         UpdPartial w = red[0];
         for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
         if (P.split_tail) {
-            P.upd_partials[blockIdx.x] = w;
+            upd_publish(P, blockIdx.x, w);
         } else {
-            UpdPartial* dstp = &P.upd_partials[blockIdx.x];
-            st_agent(&dstp->theta, w.theta);
-            st_agent(&dstp->idx, w.idx);
-            st_agent(&dstp->nonpos, w.nonpos);
-            st_agent(&dstp->T, w.T);
-            st_agent(&dstp->a_w, w.a_w);
-            st_agent(&dstp->cb_w, w.cb_w);
-            st_agent(&dstp->bix_w, w.bix_w);
+            upd_publish(P, blockIdx.x, w);
             drain_vmem();
-            const uint32_t tk = __hip_atomic_fetch_add(&st->ticket_update, 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            *s_last = (tk == gridDim.x - 1);
+            *s_last = arrive_last(arrive_group(P.arrive, ARR_UPDATE), gridDim.x, blockIdx.x);
         }
     }
     if (P.split_tail) return;  // k_tail merges after the kernel boundary
@@ -1180,7 +1194,6 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
         h->a_w = t.a_w;
         h->cb_w = t.cb_w;
         h->bix_w = t.bix_w;
-        st_agent(&st->ticket_update, 0u);
     }
 }
 
@@ -1361,14 +1374,13 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
     fold_tiles<KW>(P.B0, P.U, nf, L, c0, i0, i1, Rl);
     __syncthreads();
     if (tid == 0) {
-        const uint32_t t = __hip_atomic_fetch_add(&st->ticket_fold, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (t == gridDim.x * gridDim.y - 1);
+        s_last = arrive_last(arrive_group(P.arrive, ARR_FOLD), gridDim.x * gridDim.y,
+                             blockIdx.y * gridDim.x + blockIdx.x);
     }
     __syncthreads();
     if (s_last && tid == 0) {
         P.SY[0] = P.SY[nf];
         st->nw = 1;
-        st_agent(&st->ticket_fold, 0u);
     }
 }
 
@@ -1516,6 +1528,7 @@ __global__ void k_reset(Params P) {
         P.b_ixs[i] = ns + i;
         if (P.xw) P.xw[i] = P.b[i];  // B_w = I
     }
+    for (int64_t k = t0; k < ARR_GROUPS * ARR_LINES * ARR_STRIDE; k += stride) P.arrive[k] = 0u;
     for (int64_t j = t0; j < n; j += stride) {
         if (P.W) P.W[j] = 1.0;  // Devex reference framework
         int32_t pos = -1;
@@ -1540,10 +1553,7 @@ __global__ void k_reset(Params P) {
         st->y_applied = 0;
         st->xb_applied = 0;
         st->y_buf = 0;
-        st->ticket_price = 0;
-        st->ticket_update = 0;
         st->nw = 0;
-        st->ticket_fold = 0;
         st->leave = -1;
         st->wp = 1.0;
     }
