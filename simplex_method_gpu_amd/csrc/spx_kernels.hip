@@ -573,6 +573,11 @@ struct TailPre {
     double e_enter;  // deferred pricing tail: the entering column's reduced cost
     int32_t nw;      // eta window: pivots in the window (stable until the tail)
 };
+// the list tail depends on cnt: loaded at the start of the tail, beside the
+// partial loads, instead of as a dependent pair at kernel entry
+__device__ __forceinline__ void tail_last(const Params& P, TailPre* t) {
+    if (t && t->valid && t->kp >= 0) t->last = P.nb_list[t->cnt - 1];
+}
 
 __device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState* st, int64_t p) {
     TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
@@ -580,10 +585,7 @@ __device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState
     if (P.win) t.nw = st->nw;
     t.c_p = P.c[p];
     t.cnt = st->nb_count;
-    if (owns_col(P, p)) {
-        t.kp = P.nb_pos[p];
-        t.last = P.nb_list[t.cnt - 1];
-    }
+    if (owns_col(P, p)) t.kp = P.nb_pos[p];  // (nb_list[cnt - 1] is loaded by the tail: tail_last)
     if (P.devex) t.wp = P.W[p];
     t.valid = true;
     return t;
@@ -636,8 +638,9 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
 // vector updates are deferred (spx_device.h).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            unsigned char* smem, int nparts, const TailPre* pre = nullptr) {
+                            unsigned char* smem, int nparts, TailPre* pre = nullptr) {
     unsigned long long tm = P.stamps ? rtime() : 0;
+    if (threadIdx.x == 0) tail_last(P, pre);
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
     const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
     tm = tail_mark(P, 0, tm);
@@ -725,6 +728,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // stream takes 23 us)
     // (the explicit in-place update measured slower with its old rows loaded
     // this way: C3 59 -> 66 us, so window only)
+    // the deferred pricing partials are loaded first: vmcnt retires in issue
+    // order, so loads issued after the B prefetch would wait for all of it
+    PricePartial pw0{INFINITY, INT64_MAX, 0.0, 0.0};
+    if (P.defer_price && tid < P.price_grid) pw0 = P.price_partials[tid];
     constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
@@ -748,21 +755,23 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     int64_t p = INT64_MAX;
     int gw = 0;
     if (P.defer_price) {
-        PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
-        for (int g = tid; g < P.price_grid; g += BLOCK) {
+        PricePartial w = pw0;
+        for (int g = tid + BLOCK; g < P.price_grid; g += BLOCK) {
             const PricePartial v = P.price_partials[g];
             if (argmin_better(v.val, v.idx, w.val, w.idx)) w = v;
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const double v = __shfl_xor(w.val, off, 64);
-            const int64_t i = __shfl_xor(w.idx, off, 64);
-            const double pe = __shfl_xor(w.pad, off, 64);
-            if (argmin_better(v, i, w.val, w.idx)) { w.val = v; w.idx = i; w.pad = pe; }
-        }
+        // DPP argmin; the winner's reduced cost from its lane (cross-lane
+        // reads outside the lane-0 branch)
+        double bv = w.val;
+        int64_t bj = w.idx;
+        lane_argmin<64>(bv, bj);
+        bv = readlane_d(bv, 63);
+        bj = readlane_l(bj, 63);
+        const uint64_t hit = __ballot(w.val == bv && w.idx == bj);
+        const double be = readlane_d(w.pad, hit ? (int)__builtin_ctzll(hit) : 0);
         __shared__ PricePartial s_pw[WAVES];
-        if (lane == 0) s_pw[wave] = w;
-        __syncthreads();
+        if (lane == 0) s_pw[wave] = PricePartial{bv, bj, 0.0, be};
+        lds_barrier();  // (not __syncthreads: its vmcnt(0) would wait for the B prefetch)
         PricePartial t = s_pw[0];
         for (int i = 1; i < WAVES; ++i)
             if (argmin_better(s_pw[i].val, s_pw[i].idx, t.val, t.idx)) t = s_pw[i];
@@ -1004,7 +1013,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
     if (lane == 0) red[wave] = wp;
-    __syncthreads();
+    // only the partial crosses workgroups inside the launch (thread 0 drains
+    // it below), so the barrier waits for LDS only; the row-sharded tail
+    // reads other workgroups' alpha: full barrier
+    if constexpr (RS) __syncthreads();
+    else lds_barrier();
     if (P.split_tail) {  // k_tail merges after the kernel boundary: plain stores, no fan-in
         if (tid == 0) {
             UpdPartial w = red[0];
@@ -1020,7 +1033,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         drain_vmem();  // the partial is visible before the ticket
         *s_last = arrive_last(arrive_group(P.arrive, ARR_UPDATE), gridDim.x, blockIdx.x);
     }
-    __syncthreads();
+    if constexpr (RS) __syncthreads();
+    else lds_barrier();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
 #ifdef SPX_DIAG_SKIP_TAIL  // timing-only build: pivots stop after the first pass
