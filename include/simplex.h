@@ -157,6 +157,11 @@ typedef struct spx_opts {
                                 dw[j] and the window row of each non-basic column,
                                 FTRAN the column T_w[:, p].  Needs the window (0 =
                                 auto selects 64) and one rank; twice A's memory. */
+#define SPX_FLAG_COUNTED_TAIL 512 /* tuning: the update kernel's workgroups hand
+                                     their ratio-test partials to the tail by
+                                     drained stores + a last-arrival count
+                                     instead of tagged words polled by the
+                                     last workgroup (the default)             */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass

@@ -36,6 +36,7 @@ FLAG_NO_PERSIST = 32
 FLAG_PERSIST = 64  # force the persistent loop kernel where it applies (default: auto)
 FLAG_COMM1 = 128  # one rank through the RCCL path (tests)
 FLAG_TABLEAU = 256  # window tableau: T_w = B_w A and dw kept beside the eta window
+FLAG_COUNTED_TAIL = 512  # ratio-test hand-off by drained stores + last-arrival count (default: tagged poll)
 
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
@@ -131,7 +132,7 @@ class Context:
                  global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
                  ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0,
                  pricing: int = 0, persist: bool | None = None, loop_block: int = 0, comm1: bool = False,
-                 tableau: bool = False, trace: int = 0):
+                 tableau: bool = False, trace: int = 0, counted_tail: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -148,7 +149,8 @@ class Context:
                    | (FLAG_GLOBAL_Y if global_y else 0) | (FLAG_ROW_SHARD if row_shard else 0)
                    | (FLAG_SPLIT_TAIL if split_tail else 0)
                    | ({None: 0, True: FLAG_PERSIST, False: FLAG_NO_PERSIST}[persist])
-                   | (FLAG_COMM1 if comm1 else 0) | (FLAG_TABLEAU if tableau else 0))
+                   | (FLAG_COMM1 if comm1 else 0) | (FLAG_TABLEAU if tableau else 0)
+                   | (FLAG_COUNTED_TAIL if counted_tail else 0))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)

@@ -422,6 +422,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.price_partials, (size_t)pc.grid));
     P.upd_cap = uc.grid;
     SPX_TRY(x->alloc(&P.upd_soa, (size_t)(7 * uc.grid)));
+    if (!P.row_shard && !P.tab && !(x->opts.flags & SPX_FLAG_COUNTED_TAIL))
+        SPX_TRY(x->alloc(&P.upd_tag, (size_t)(UPD_WORDS * uc.grid)));
     // the persistent loop kernel replaces the two-kernel pass where it applies
     if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
@@ -656,6 +658,7 @@ int read_state(spx_ctx* x) {
     x->status = x->st_host->status;  // ST_RUNNING == SPX_STATUS_MAX_ITER
     x->nw = x->st_host->nw;
     if (x->status == ST_WINDOW_FULL) return fail(SPX_ERR_STATE, "internal error: eta window overflow");
+    if (x->status == ST_HANDOFF_TIMEOUT) return fail(SPX_ERR_STATE, "internal error: ratio-test hand-off timed out");
     return SPX_OK;
 }
 

@@ -58,7 +58,7 @@
 
 namespace spx {
 
-enum : int32_t { ST_RUNNING = 0, ST_OPTIMAL = 1, ST_UNBOUNDED = 2, ST_WINDOW_FULL = 16 };
+enum : int32_t { ST_RUNNING = 0, ST_OPTIMAL = 1, ST_UNBOUNDED = 2, ST_WINDOW_FULL = 16, ST_HANDOFF_TIMEOUT = 17 };
 
 // (value, global index) candidate; the order is value, then smallest index —
 // cub::DeviceReduce::ArgMin's first-index semantics (v4:294,324) for every
@@ -113,6 +113,8 @@ constexpr int ARR_SHARDS = 8;
 constexpr int ARR_STRIDE = 32;  // uint32 per 128-byte line
 constexpr int ARR_LINES = 1 + ARR_SHARDS;
 enum : int { ARR_PRICE = 0, ARR_UPDATE = 1, ARR_FOLD = 2, ARR_GROUPS = 3 };
+// tagged ratio-test partial: 7 eight-byte fields as 14 {32-bit half, tag} words
+constexpr int UPD_WORDS = 14;
 
 struct alignas(16) DevState {
     int32_t status;      // ST_*
@@ -174,6 +176,10 @@ struct Params {
                                    // (the window appends Wt[p][0..KW) to the head)
     double* upd_soa;               // k_update partials, field-major (upd_publish)
     int64_t upd_cap;               // workgroup slots per field
+    // k_update partials as tagged words (UPD_WORDS per slot, field-major),
+    // polled by the last workgroup instead of a drain + last-arrival count;
+    // nullptr: the counted hand-off (upd_soa + arrive)
+    uint64_t* upd_tag;
     DevState* st;
     // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
     // global rows [r0, r0 + mloc) of B^-1, stored as B0/B1 (mloc x L ping-pong)

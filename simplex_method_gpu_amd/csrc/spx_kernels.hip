@@ -508,17 +508,92 @@ __device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g) {
     return v;
 }
 
+// Tagged hand-off (P.upd_tag, the default on replicated B^-1): wave 0 of every
+// workgroup publishes its partial as UPD_WORDS 8-byte granules {32-bit half,
+// tag} with one sc1 store instruction (lane l = word l; field-major, so the
+// poll's loads coalesce), and the last workgroup polls each slot until all
+// its words carry this pass's tag (MI355X_MICROARCH.md, handoff-1to1).  The
+// slowest workgroup's partial then reaches the tail in one one-way hop; the
+// counted form (upd_soa + arrive_last) pays a store drain and two atomic
+// round trips first.  The tail clears every slot it consumed, so a slot holds
+// a live tag only between its publish and the tail of the same pass.
+__device__ __forceinline__ uint64_t upd_field_bits(const UpdPartial& w, int f) {
+    switch (f) {
+        case 0: return (uint64_t)__double_as_longlong(w.theta);
+        case 1: return (uint64_t)w.idx;
+        case 2: return (uint64_t)w.nonpos;
+        case 3: return (uint64_t)__double_as_longlong(w.T);
+        case 4: return (uint64_t)__double_as_longlong(w.a_w);
+        case 5: return (uint64_t)__double_as_longlong(w.cb_w);
+        default: return (uint64_t)w.bix_w;
+    }
+}
+__device__ __forceinline__ void upd_publish_tagged(const Params& P, int g, const UpdPartial& w, uint32_t tag,
+                                                   int lane) {
+    if (lane < UPD_WORDS) {
+        const uint64_t u = upd_field_bits(w, lane >> 1);
+        const uint32_t half = (lane & 1) ? (uint32_t)(u >> 32) : (uint32_t)u;
+        st_agent(&P.upd_tag[(int64_t)lane * P.upd_cap + g], ((uint64_t)tag << 32) | half);
+    }
+}
+// Poll slot g until its UPD_WORDS words carry tag; false after ~2^20 rounds.
+__device__ __forceinline__ bool upd_poll_tagged(const Params& P, int g, uint32_t tag, UpdPartial& v) {
+    uint64_t w[UPD_WORDS];
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < UPD_WORDS; ++k) w[k] = ld_agent(&P.upd_tag[(int64_t)k * P.upd_cap + g]);
+#pragma unroll
+        for (int k = 0; k < UPD_WORDS; ++k) ok = ok && (uint32_t)(w[k] >> 32) == tag;
+        if (ok) break;
+        if (spins > (1u << 20)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    uint64_t f[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) f[k] = (w[2 * k] & 0xffffffffull) | (w[2 * k + 1] << 32);
+    v.theta = __longlong_as_double((long long)f[0]);
+    v.idx = (int64_t)f[1];
+    v.nonpos = (int64_t)f[2];
+    v.T = __longlong_as_double((long long)f[3]);
+    v.a_w = __longlong_as_double((long long)f[4]);
+    v.cb_w = __longlong_as_double((long long)f[5]);
+    v.bix_w = (int64_t)f[6];
+    v.pad = 0;
+    return true;
+}
+__device__ __forceinline__ void upd_clear_tagged(const Params& P, int g) {
+#pragma unroll
+    for (int k = 0; k < UPD_WORDS; ++k) P.upd_tag[(int64_t)k * P.upd_cap + g] = 0ull;
+}
+
 // Leaving argmin over the k_update workgroup partials + unbounded count
 // (v4:317-325), carrying the winner's scalars.  One dependent round trip
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
 // order is fixed for a given launch geometry.
 template <int BLOCK>
-__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts) {
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag = 0,
+                                             bool* timed_out = nullptr) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // every slot's seven fields are loaded before any is used (one round trip)
-    UpdPartial w = (tid < nparts) ? upd_fetch(P, tid) : upd_empty();
-    for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch(P, g));
+    UpdPartial w = upd_empty();
+    if (tag) {  // tagged hand-off: poll, then clear the consumed slots
+        bool ok = true;
+        for (int g = tid; g < nparts; g += BLOCK) {
+            UpdPartial v;
+            if (!upd_poll_tagged(P, g, tag, v)) {
+                ok = false;
+                break;
+            }
+            upd_merge(w, v);
+            upd_clear_tagged(P, g);
+        }
+        if (!ok) *timed_out = true;  // (a benign race: every writer stores true)
+    } else {
+        // every slot's seven fields are loaded before any is used (one round trip)
+        w = (tid < nparts) ? upd_fetch(P, tid) : upd_empty();
+        for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch(P, g));
+    }
     // wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
     // winner's scalars come from its lane by readlane
     double th = w.theta;
@@ -638,13 +713,20 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
 // vector updates are deferred (spx_device.h).
 template <int BLOCK>
 __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min_e, int64_t it,
-                            unsigned char* smem, int nparts, TailPre* pre = nullptr) {
+                            unsigned char* smem, int nparts, TailPre* pre = nullptr, uint32_t tag = 0) {
     unsigned long long tm = P.stamps ? rtime() : 0;
     if (threadIdx.x == 0) tail_last(P, pre);
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + UpdLds<BLOCK>::red);
-    const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts);
+    __shared__ bool s_to;
+    if (threadIdx.x == 0) s_to = false;
+    if (tag) lds_barrier();
+    const UpdPartial t = reduce_update_partials<BLOCK>(P, red, nparts, tag, &s_to);
     tm = tail_mark(P, 0, tm);
     if (threadIdx.x != 0) return;
+    if (tag && s_to) {  // a partial never arrived (a fault elsewhere): stop loudly
+        st->status = ST_HANDOFF_TIMEOUT;
+        return;
+    }
     const int64_t q = t.idx;
     if (t.nonpos == P.m || q < 0 || q >= P.m) {
         // every alpha_i <= 0: Unbounded (v4:319-322).  A ratio test with no
@@ -1024,6 +1106,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
             upd_publish(P, blockIdx.x, w);
         }
+        return;
+    }
+    if (!RS && P.upd_tag) {  // tagged hand-off to the last workgroup (upd_publish_tagged)
+        const uint32_t tag = (uint32_t)(it + 1);
+        if (wave == 0) {
+            UpdPartial w = red[0];
+            for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
+            upd_publish_tagged(P, blockIdx.x, w, tag, lane);
+        }
+        if (blockIdx.x != gridDim.x - 1) return;
+        const unsigned long long t_tail = slot ? rtime() : 0;
+        update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre, tag);
+        stamp_tail(slot, t_tail, win);
         return;
     }
     if (tid == 0) {
@@ -1543,6 +1638,8 @@ __global__ void k_reset(Params P) {
         if (P.xw) P.xw[i] = P.b[i];  // B_w = I
     }
     for (int64_t k = t0; k < ARR_GROUPS * ARR_LINES * ARR_STRIDE; k += stride) P.arrive[k] = 0u;
+    if (P.upd_tag)
+        for (int64_t k = t0; k < UPD_WORDS * P.upd_cap; k += stride) P.upd_tag[k] = 0ull;
     for (int64_t j = t0; j < n; j += stride) {
         if (P.W) P.W[j] = 1.0;  // Devex reference framework
         int32_t pos = -1;
