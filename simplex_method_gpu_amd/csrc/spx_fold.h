@@ -3,13 +3,26 @@
 // update B += U R of a 64-column stripe of a row-major matrix with fp64 MFMA
 // tiles (v_mfma_f64_16x16x4f64), R rebuilt from base rows and coefficients.
 //
-// Workgroup shape (tools/fold_bench.hip, MI355X, m = 4096, KW = 64: 168 ->
-// 80 us, bit-identical):
+// Workgroup shape (FOLD_THREADS = 512, one per CU; tools/fold2_bench.hip,
+// MI355X, m = 4096, KW = 64, MALL flushed: 95 -> 76 us, bit-identical):
+//   0. every wave's first tile (B rows and U fragment) is loaded before
+//      anything else, so HBM is busy during the rebuild (fold_tile_first);
 //   1. the coefficients are staged transposed into LDS (fold_stage_N);
-//   2. wave 0 rebuilds R right-looking (fold_rebuild_R);
+//   2. waves 0-3 rebuild R right-looking, a quad of lanes per column
+//      (fold_rebuild_R4);
 //   3. every wave walks its 16-row tiles (fold_tiles), R fragments read from
-//      LDS per k-step rather than held in 128 VGPRs, the next tile's loads
-//      issued before this tile's MFMAs.
+//      LDS per k-step, the next tile's U fragment and B rows loaded after
+//      this tile's operands.
+//
+// Column map.  The MFMA accumulator of block jb holds, in lane (kr, cl), rows
+// kr + 4 r (r = 0..3) and one column per cl.  Block jb, column cl stands for
+// stripe column fold_col(jb, cl) = 32 (jb >> 1) + 2 cl + (jb & 1), so a lane's
+// blocks 2h and 2h + 1 are two adjacent columns: the B tile moves as 16-byte
+// loads and stores of 16 lanes x 16 B = 256 contiguous bytes per row (6.5
+// TB/s on the fold's footprint) instead of 8-byte accesses of 128 B per row
+// (1.9-3.0 TB/s).  R is stored in Rl in the same permuted order
+// (fold_slot), and only the N dimension is permuted, so every sum keeps its
+// order and the bits do not change.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,14 +30,21 @@
 namespace spx {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double fdbl2 __attribute__((ext_vector_type(2)));
 
 template <int KW>
 constexpr int FOLD_NP = KW + 2;  // LDS pitch of the staged coefficients
+// LDS pitch of Rl: 72 doubles put the four k-rows of an MFMA operand read on
+// different banks (fold2_bench: -2 % against 64)
+constexpr int FOLD_RP = 72;
+
+// stripe column of MFMA block jb, accumulator column cl, and its inverse
+__host__ __device__ constexpr int fold_col(int jb, int cl) { return 32 * (jb >> 1) + 2 * cl + (jb & 1); }
+__host__ __device__ constexpr int fold_slot(int c) { return 16 * (2 * (c >> 5) + (c & 1)) + ((c >> 1) & 15); }
 
 // All threads: NT[s][t] = Urows[t][s] on the strict lower nf x nf triangle, 0
 // elsewhere (so rows t >= nf of R rebuild to exact zeros).  Pitch KW + 2 keeps
-// the transposing stores off one bank and the rows 16-byte aligned (the
-// rebuild's uniform reads pair up into ds_read_b128).
+// the transposing stores off one bank and the rows 16-byte aligned.
 template <int KW>
 __device__ __forceinline__ void fold_stage_N(const double* Urows, int nf, double (&NT)[KW][FOLD_NP<KW>]) {
     for (int k = threadIdx.x; k < KW * KW; k += blockDim.x) {
@@ -33,87 +53,188 @@ __device__ __forceinline__ void fold_stage_N(const double* Urows, int nf, double
     }
 }
 
-// Wave 0 of a fold workgroup, after fold_stage_N and a barrier: r_t for the
-// 64-column stripe at c0 (one column per lane), r_t = Qrows[t] + sum_{s<t}
-// Urows[t][s] r_s, into Rl and R.  Right-looking: once r_s is final every later
-// r_t takes its s term, so each r_t still sums s = 0, 1, .. in order (the bits
-// of the left-looking recurrence) but the 63 accumulators are independent
-// instead of one 2016-deep fma chain.
-template <int KW>
-__device__ __forceinline__ void fold_rebuild_R(const double* Qrows, const double (&NT)[KW][FOLD_NP<KW>], int nf, int64_t L,
-                                               int64_t c0, double (&Rl)[KW][64], double (&R)[KW]) {
+// DPP quad_perm of a double (both halves)
+template <int CTRL>
+__device__ __forceinline__ double quad_dpp(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)b, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// Waves 0-3 of a fold workgroup (threadIdx.x < 256), after fold_stage_N
+// and a barrier: r_t = Qrows[t] + sum_{s<t} Urows[t][s] r_s for the 64-column
+// stripe at c0, into Rl (columns in fold_slot order).  Lane 4 jj + g of wave
+// w owns stripe column 16 w + jj and rows t = g, g + 4, ..  Right-looking:
+// once r_s is final every later r_t takes its s term, so each r_t sums s = 0,
+// 1, .. in order (the bits of the left-looking recurrence); a step's 63 - s
+// updates are spread over the quad's 4 lanes and the owner of row s hands r_s
+// to its quad by DPP.  (One wave doing 64 columns alone was bound by its LDS
+// operand latency: ~28 us of a C3 fold; this form 21-24 us with the loads.)
+template <int KW, int RP>
+__device__ __forceinline__ void fold_rebuild_R4(const double* Qrows, const double (&NT)[KW][FOLD_NP<KW>], int nf,
+                                                int64_t L, int64_t c0, double (&Rl)[KW][RP]) {
+    constexpr int TG = KW / 4;
     const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane & 3;
+    const int col = 16 * wave + (lane >> 2);
+    const int slot = fold_slot(col);
+    double R[TG];  // R[u]: row 4 u + g
 #pragma unroll
-    for (int t = 0; t < KW; ++t) R[t] = (t < nf) ? Qrows[(int64_t)t * L + c0 + lane] : 0.0;
+    for (int u = 0; u < TG; ++u) {
+        const int t = 4 * u + g;
+        R[u] = (t < nf) ? Qrows[(int64_t)t * L + c0 + col] : 0.0;
+    }
 #pragma unroll
     for (int s = 0; s < KW; ++s) {
-        Rl[s][lane] = R[s];
+        const int us = s >> 2;
+        double rs;
+        switch (s & 3) {  // r_s from the quad lane that owns row s
+            case 0: rs = quad_dpp<0x00>(R[us]); break;
+            case 1: rs = quad_dpp<0x55>(R[us]); break;
+            case 2: rs = quad_dpp<0xAA>(R[us]); break;
+            default: rs = quad_dpp<0xFF>(R[us]); break;
+        }
+        if (g == (s & 3)) Rl[s][slot] = R[us];
+        // row 4 us + g > s only in the quad lanes past the owner
+        if (g > (s & 3)) R[us] = fma(NT[s][4 * us + g], rs, R[us]);
 #pragma unroll
-        for (int t = s + 1; t < KW; ++t) R[t] = fma(NT[s][t], R[s], R[t]);
+        for (int u = us + 1; u < TG; ++u) R[u] = fma(NT[s][4 * u + g], rs, R[u]);
     }
 }
 
 // The 16-row x 64-column tile of B at rows r0.. (rows >= i1 read as 0), in the
-// MFMA accumulator layout: lane holds rows r0 + kr + 4 r, column 16 jb + cl.
+// MFMA accumulator layout under the column map: lane (kr, cl) holds rows
+// r0 + kr + 4 r, columns fold_col(jb, cl).  8 loads of 16 B per lane.
 __device__ __forceinline__ void fold_tile_load(const double* B, int64_t L, int64_t c0, int64_t r0, int64_t i1,
                                                dbl4 (&t)[4]) {
     const int lane = threadIdx.x & 63;
     const int kr = lane >> 4, cl = lane & 15;
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = r0 + kr + 4 * r;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t i = r0 + kr + 4 * r;
-            t[jb][r] = (i < i1) ? B[i * L + c0 + 16 * jb + cl] : 0.0;
+        for (int h = 0; h < 2; ++h) {
+            fdbl2 v = {0.0, 0.0};
+            if (i < i1) v = *reinterpret_cast<const fdbl2*>(&B[i * L + c0 + 32 * h + 2 * cl]);
+            t[2 * h][r] = v.x;
+            t[2 * h + 1][r] = v.y;
         }
+    }
+}
+__device__ __forceinline__ void fold_tile_store(double* B, int64_t L, int64_t c0, int64_t r0, int64_t i1,
+                                                const dbl4 (&t)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i = r0 + kr + 4 * r;
+        if (i < i1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                fdbl2 v;
+                v.x = t[2 * h][r];
+                v.y = t[2 * h + 1][r];
+                *reinterpret_cast<fdbl2*>(&B[i * L + c0 + 32 * h + 2 * cl]) = v;
+            }
+        }
+    }
 }
 
-// B[i0:i1, c0:c0+64] += U[i0:i1, 0:nf] R[0:nf, stripe] with 16x16 fp64 MFMA
-// tiles (the B tile is the accumulator); U is m x KW row-major.  Wave w takes
-// tiles i0 + 16 w, i0 + 16 (w + nwaves), ..  Call after a barrier that
-// published Rl.
+// U fragment (MFMA A operand) of the tile at rows r0..: lane holds
+// U[r0 + cl][4 s2 + kr] (0 past i1 or nf).
 template <int KW>
+__device__ __forceinline__ void fold_ufrag_load(const double* U, int nf, int64_t r0, int64_t i1,
+                                                double (&af)[KW / 4]) {
+    const int lane = threadIdx.x & 63;
+    const int kr = lane >> 4, cl = lane & 15;
+    const int64_t ia = r0 + cl;
+#pragma unroll
+    for (int s2 = 0; s2 < KW / 4; ++s2) {
+        const int t = 4 * s2 + kr;
+        af[s2] = (ia < i1 && t < nf) ? U[ia * KW + t] : 0.0;
+    }
+}
+
+// A wave's first tile (B rows and U fragment), loaded before the R rebuild.
+template <int KW>
+struct FoldTilePre {
+    dbl4 b[4];
+    double u[KW / 4];
+};
+template <int KW>
+__device__ __forceinline__ void fold_tile_first(const double* B, const double* U, int nf, int64_t L, int64_t c0,
+                                                int64_t i0, int64_t i1, FoldTilePre<KW>& pre) {
+    const int64_t r0 = i0 + 16 * (int64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (r0 >= i1) return;
+    fold_ufrag_load<KW>(U, nf, r0, i1, pre.u);
+    fold_tile_load(B, L, c0, r0, i1, pre.b);
+}
+
+// B[i0:i1, stripe c0] += U[i0:i1, 0:nf] R[0:nf, stripe] with 16x16 fp64 MFMA
+// tiles (the B tile is the accumulator); U is m x KW row-major.  Wave w takes
+// tiles i0 + 16 w, i0 + 16 (w + nwaves), ..  The next tile's U fragment and B
+// rows are issued after this tile's operands were taken: vmcnt retires in
+// issue order, and U fragments loaded per tile after the next tile's B loads
+// (the previous form) made every tile's MFMAs wait for that whole prefetch.
+// first: the wave's first tile (fold_tile_first) when have_first.  Call
+// after a barrier that published Rl.
+template <int KW, int RP>
 __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, int64_t L, int64_t c0, int64_t i0,
-                                           int64_t i1, const double (&Rl)[KW][64]) {
+                                           int64_t i1, const double (&Rl)[KW][RP], const FoldTilePre<KW>& first,
+                                           bool have_first) {
     constexpr int KS = KW / 4;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwaves = blockDim.x >> 6;
     const int kr = lane >> 4, cl = lane & 15;
-    const int ks = (nf + 3) / 4;
-    dbl4 nxt[4];
-    if (i0 + 16 * wave < i1) fold_tile_load(B, L, c0, i0 + 16 * wave, i1, nxt);
-    for (int64_t r0 = i0 + 16 * wave; r0 < i1; r0 += 16 * nwaves) {
-        dbl4 acc[4];
+    int64_t r0 = i0 + 16 * wave;
+    if (r0 >= i1) return;
+    dbl4 nb[4];
+    double nu[KS];
+    if (have_first) {
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) acc[jb] = nxt[jb];
-        const int64_t rn = r0 + 16 * nwaves;
-        if (rn < i1) fold_tile_load(B, L, c0, rn, i1, nxt);
-        // U fragment (A operand): lane holds U[r0 + cl][4 s + kr]
-        const int64_t ia = r0 + cl;
+        for (int jb = 0; jb < 4; ++jb) nb[jb] = first.b[jb];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) nu[s2] = first.u[s2];
+    } else {
+        fold_ufrag_load<KW>(U, nf, r0, i1, nu);
+        fold_tile_load(B, L, c0, r0, i1, nb);
+    }
+    for (; r0 < i1; r0 += 16 * nwaves) {
+        dbl4 acc[4];
         double af[KS];
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            const int t = 4 * s2 + kr;
-            af[s2] = (ia < i1 && t < nf) ? U[ia * KW + t] : 0.0;
+        for (int jb = 0; jb < 4; ++jb) acc[jb] = nb[jb];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) af[s2] = nu[s2];
+        const int64_t rn = r0 + 16 * nwaves;
+        if (rn < i1) {
+            fold_ufrag_load<KW>(U, nf, rn, i1, nu);
+            fold_tile_load(B, L, c0, rn, i1, nb);
         }
-        // R fragment (B operand) from LDS: R[4 s + kr][16 jb + cl]
+        // R fragment (B operand) from LDS: R[4 s2 + kr][slot 16 jb + cl].  All
+        // KS k-steps run (rows t >= nf of R and U's columns past nf are exact
+        // zeros; a per-step nf branch kept the next step's LDS reads behind
+        // this step's MFMAs), one step's fragments read ahead: the schedule
+        // barrier keeps the compiler from hoisting every step's reads (256
+        // VGPRs, one workgroup per CU) or exposing each read's latency.
+        double rf[2][4];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) rf[0][jb] = Rl[kr][16 * jb + cl];
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
-            if (s2 < ks) {
+            if (s2 + 1 < KS) {
 #pragma unroll
-                for (int jb = 0; jb < 4; ++jb)
-                    acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], Rl[4 * s2 + kr][16 * jb + cl], acc[jb], 0,
-                                                                   0, 0);
+                for (int jb = 0; jb < 4; ++jb) rf[(s2 + 1) & 1][jb] = Rl[4 * (s2 + 1) + kr][16 * jb + cl];
             }
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb)
+                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], rf[s2 & 1][jb], acc[jb], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t i = r0 + kr + 4 * r;
-                if (i < i1) B[i * L + c0 + 16 * jb + cl] = acc[jb][r];
-            }
+        fold_tile_store(B, L, c0, r0, i1, acc);
     }
 }
 
@@ -124,11 +245,16 @@ __device__ __forceinline__ void fold_rows(int64_t m, int64_t& i0, int64_t& i1) {
     i1 = (i0 + per < m) ? i0 + per : m;
 }
 
-// Host: the row split of a fold grid over nx stripes — about 2 workgroups per
-// CU (65 KiB of LDS each), at least one 16-row tile per wave.
+// Fold workgroups: 8 waves, one workgroup per CU (~70 KiB of LDS): waves
+// 0-3 rebuild R (fold_rebuild_R4) while 4-7 hold their first tiles, then all
+// eight walk tiles (fold2_bench, C3: 75.8 us against 81-84 us for 4-wave
+// workgroups at 1 or 2 per CU).
+constexpr int FOLD_THREADS = 512;
+// Host: the row split of a fold grid over nx stripes — about one workgroup
+// per CU, at least one 16-row tile per wave.
 inline int64_t fold_grid_y(int64_t m, int nx, int cus) {
-    int64_t ny = ((int64_t)2 * cus + nx - 1) / nx;
-    const int64_t maxy = (m + 63) / 64;
+    int64_t ny = ((int64_t)cus + nx - 1) / nx;
+    const int64_t maxy = (m + 16 * (FOLD_THREADS / 64) - 1) / (16 * (FOLD_THREADS / 64));
     if (ny > maxy) ny = maxy;
     if (ny < 1) ny = 1;
     return ny;

@@ -79,7 +79,7 @@ __device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned lo
         const unsigned long long b = __hip_atomic_load(&win[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long e = __hip_atomic_load(&win[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicAdd(&win[2], b - t0);
-        atomicAdd(&win[3], t_tail - e);
+        atomicAdd(&win[3], t_tail > e ? t_tail - e : 0ull);  // (tagged hand-off: the tail may start first)
         __hip_atomic_store(&win[0], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&win[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1436,12 +1436,12 @@ __global__ __launch_bounds__(256) void k_finalize_rs(Params P) {
 // for 2).
 // ---------------------------------------------------------------------------
 template <int KW>
-__global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
+__global__ __launch_bounds__(FOLD_THREADS) void k_fold(Params P, int min_nw) {
     DevState* st = P.st;
     const int nw = st->nw;
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
-    __shared__ double Rl[KW][64];
+    __shared__ double Rl[KW][FOLD_RP];
     __shared__ double NT[KW][FOLD_NP<KW>];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1450,19 +1450,23 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
     const int64_t c0 = (int64_t)blockIdx.x * 64;
     int64_t i0, i1;
     fold_rows(P.m, i0, i1);
+    // spx_fold.h: first tiles in flight, R rebuilt by all four waves, tiles
+    FoldTilePre<KW> pre;
+    fold_tile_first<KW>(P.B0, P.U, nf, L, c0, i0, i1, pre);
     fold_stage_N<KW>(P.Urows, nf, NT);
     __syncthreads();
-    if (wave == 0) {
-        double R[KW];
-        fold_rebuild_R<KW>(P.Qrows, NT, nf, L, c0, Rl, R);
-        if (blockIdx.y == 0) {
-            double* y = st->y_buf ? P.y1 : P.y0;
-            double d = 0.0;
+    if (tid < 256) fold_rebuild_R4<KW, FOLD_RP>(P.Qrows, NT, nf, L, c0, Rl);
+    __syncthreads();
+    fold_tiles<KW, FOLD_RP>(P.B0, P.U, nf, L, c0, i0, i1, Rl, pre, true);
+    if (wave == 0 && blockIdx.y == 0) {
+        // y_w += SY R for this stripe (t ascending, the rebuild's R)
+        double* y = st->y_buf ? P.y1 : P.y0;
+        const int sl = fold_slot(lane);
+        double d = 0.0;
 #pragma unroll
-            for (int t = 0; t < KW; ++t)
-                if (t < nf) d = fma(P.SY[t], R[t], d);
-            y[c0 + lane] += d;
-        }
+        for (int t = 0; t < KW; ++t)
+            if (t < nf) d = fma(P.SY[t], Rl[t][sl], d);
+        y[c0 + lane] += d;
     } else if (wave == 1) {
         // xw = B_w b follows B_w: xw += U (R b), R b = Wt[n][0..nf); the rows
         // spread over every workgroup, one lane per row, t ascending
@@ -1479,8 +1483,6 @@ __global__ __launch_bounds__(256) void k_fold(Params P, int min_nw) {
             P.xw[i] += d;
         }
     }
-    __syncthreads();
-    fold_tiles<KW>(P.B0, P.U, nf, L, c0, i0, i1, Rl);
     __syncthreads();
     if (tid == 0) {
         s_last = arrive_last(arrive_group(P.arrive, ARR_FOLD), gridDim.x * gridDim.y,
@@ -1765,10 +1767,10 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     const int nx = (int)(P.L / 64);
     const dim3 grid((unsigned)nx, (unsigned)fold_grid_y(P.m, nx, cus));
     switch (P.win) {
-        case 8: hipLaunchKernelGGL(k_fold<8>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 16: hipLaunchKernelGGL(k_fold<16>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 32: hipLaunchKernelGGL(k_fold<32>, grid, dim3(256), 0, s, P, min_nw); break;
-        case 64: hipLaunchKernelGGL(k_fold<64>, grid, dim3(256), 0, s, P, min_nw); break;
+        case 8: hipLaunchKernelGGL(k_fold<8>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_fold<16>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_fold<32>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_fold<64>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -192,22 +192,21 @@ __global__ __launch_bounds__(256) void k_rv_step(RvParams R, int tau, const doub
     if (tau + 1 < R.nb) rv_select(R, tau + 1, ok, nextv, freerow, i);
 }
 
-__global__ __launch_bounds__(256) void k_rv_fold(RvParams R) {
+__global__ __launch_bounds__(FOLD_THREADS) void k_rv_fold(RvParams R) {
     if (R.rs->singular) return;
-    __shared__ double Rl[RV_NB][64];
+    __shared__ double Rl[RV_NB][FOLD_RP];
     __shared__ double NT[RV_NB][FOLD_NP<RV_NB>];
     const int64_t L = R.L;
     const int64_t c0 = (int64_t)blockIdx.x * 64;
     int64_t i0, i1;
     fold_rows(R.m, i0, i1);
+    FoldTilePre<RV_NB> pre;
+    fold_tile_first<RV_NB>(R.X, R.U, R.nb, L, c0, i0, i1, pre);
     fold_stage_N<RV_NB>(R.Urows, R.nb, NT);
     __syncthreads();
-    if ((threadIdx.x >> 6) == 0) {
-        double Rr[RV_NB];
-        fold_rebuild_R<RV_NB>(R.Qrows, NT, R.nb, L, c0, Rl, Rr);
-    }
+    if (threadIdx.x < 256) fold_rebuild_R4<RV_NB, FOLD_RP>(R.Qrows, NT, R.nb, L, c0, Rl);
     __syncthreads();
-    fold_tiles<RV_NB>(R.X, R.U, R.nb, L, c0, i0, i1, Rl);
+    fold_tiles<RV_NB, FOLD_RP>(R.X, R.U, R.nb, L, c0, i0, i1, Rl, pre, true);
 }
 
 // B^-1[owner[q],:] = X[q,:]
@@ -312,7 +311,7 @@ hipError_t rv_launch_step(const RvParams& R, int tau, const double* Pin, double*
 
 hipError_t rv_launch_fold(const RvParams& R, int cus, hipStream_t s) {
     const int nx = (int)(R.L / 64);
-    hipLaunchKernelGGL(k_rv_fold, dim3((unsigned)nx, (unsigned)fold_grid_y(R.m, nx, cus)), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(k_rv_fold, dim3((unsigned)nx, (unsigned)fold_grid_y(R.m, nx, cus)), dim3(FOLD_THREADS), 0, s, R);
     return hipGetLastError();
 }
 
