@@ -51,7 +51,7 @@ def main():
         wr = 1024.0 * statistics.median(wv)
         out[k] = {"launches": len(fv), "read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                   "raw_fetch_kib_median": statistics.median(fv), "raw_write_kib_median": statistics.median(wv)}
-        if "fold" in k:  # 8-byte-per-lane tile loads: the x2 stream correction may not hold
+        if k == "k_tab_fold":  # 8-byte-per-lane tile loads: the x2 stream correction may not hold
             out[k]["note"] = "8 B/lane loads: read_bytes assumes the x2 correction; raw x1 = %.0f" % (
                 1024.0 * statistics.median(fv))
     if "k_price" in out:
