@@ -162,6 +162,10 @@ typedef struct spx_opts {
                                      drained stores + a last-arrival count
                                      instead of tagged words polled by the
                                      last workgroup (the default)             */
+#define SPX_FLAG_PRICE_TAIL 1024 /* tuning: the pricing kernel's last workgroup
+                                    merges the entering candidates (default on
+                                    one rank with the window: every update
+                                    workgroup merges k_price's partials)     */
 #define SPX_FLAG_ROW_SHARD 8 /* nranks > 1: B^-1 row-sharded over the ranks
                                 (ceil(m/nranks) rows each) instead of
                                 replicated; one extra all-gather per pass
@@ -281,8 +285,11 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
  * update body, update tail; out[4..8] = update-tail sub-phases (partials ->
  * q, s_y dot, block sum, bookkeeping, -); out[9..12] = update prologue
  * (earliest workgroup start -> earliest row stream start), update drain
- * (latest stream end -> last ticket), price prologue, price drain.  Resets. */
-#define SPX_PHASES 13
+ * (latest stream end -> last ticket), price prologue, price drain;
+ * out[13..17] = the update kernel's workgroup 0, from its start to: status
+ * read, entering column known, row stream start, its wave 0's stream end,
+ * partial published.  Resets. */
+#define SPX_PHASES 18
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
 /* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]

@@ -37,6 +37,7 @@ FLAG_PERSIST = 64  # force the persistent loop kernel where it applies (default:
 FLAG_COMM1 = 128  # one rank through the RCCL path (tests)
 FLAG_TABLEAU = 256  # window tableau: T_w = B_w A and dw kept beside the eta window
 FLAG_COUNTED_TAIL = 512  # ratio-test hand-off by drained stores + last-arrival count (default: tagged poll)
+FLAG_PRICE_TAIL = 1024  # k_price's last workgroup merges the entering candidates (default: deferred into k_update)
 
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
@@ -132,7 +133,8 @@ class Context:
                  global_y: bool = False, row_shard: bool = False, split_tail: bool = False, window: int = 0,
                  ratio_test: int = 0, piv_tol: float = 1e-9, feas_tol: float = 1e-9, refactor_every: int = 0,
                  pricing: int = 0, persist: bool | None = None, loop_block: int = 0, comm1: bool = False,
-                 tableau: bool = False, trace: int = 0, counted_tail: bool = False):
+                 tableau: bool = False, trace: int = 0, counted_tail: bool = False,
+                 price_tail: bool = False):
         L = load()
         o = SpxOpts()
         L.spx_default_opts(ctypes.byref(o))
@@ -150,7 +152,7 @@ class Context:
                    | (FLAG_SPLIT_TAIL if split_tail else 0)
                    | ({None: 0, True: FLAG_PERSIST, False: FLAG_NO_PERSIST}[persist])
                    | (FLAG_COMM1 if comm1 else 0) | (FLAG_TABLEAU if tableau else 0)
-                   | (FLAG_COUNTED_TAIL if counted_tail else 0))
+                   | (FLAG_COUNTED_TAIL if counted_tail else 0) | (FLAG_PRICE_TAIL if price_tail else 0))
         h = ctypes.c_void_p()
         if A_cols is not None:
             A_cols = np.ascontiguousarray(A_cols, dtype=np.float64)
@@ -273,13 +275,17 @@ class Context:
 
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""
-        out = (ctypes.c_double * 13)()
+        out = (ctypes.c_double * 18)()
         check(self._L.spx_phase_times(self._h, out))
         return {"price_body_us": out[0], "price_tail_us": out[1],
                 "update_body_us": out[2], "update_tail_us": out[3],
                 "tail_partials_us": out[4], "tail_sy_us": out[5], "tail_blocksum_us": out[6],
                 "tail_bookkeeping_us": out[7], "update_prologue_us": out[9], "update_drain_us": out[10],
-                "price_prologue_us": out[11], "price_drain_us": out[12]}
+                "price_prologue_us": out[11], "price_drain_us": out[12],
+                # k_update workgroup 0, since its start: status checked, entering
+                # column reduced, row scalars issued, its wave 0 stream done,
+                # its partial published
+                "upd_wg0_us": [round(out[13 + k], 2) for k in range(5)]}
 
     def loop_times(self):
         """Persistent loop kernel (timing=True): launch ms + passes (hipEvents)

@@ -485,7 +485,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // in flight when k_update reduces the partials), C2 explicit 24.9 -> 23.2
     // us; C3 explicit 126.5 -> 128.5 us (its stream waits for the reduction),
     // so not for large explicit passes
-    x->defer_ok = (P.win || m <= 2048) && !x->use_comm && !P.split_tail && !P.row_shard && !(x->opts.flags & SPX_FLAG_STAMPS);
+    x->defer_ok = (P.win || m <= 2048) && !x->use_comm && !P.split_tail && !P.row_shard &&
+                  !(x->opts.flags & (SPX_FLAG_STAMPS | SPX_FLAG_PRICE_TAIL));
     P.price_out = x->send;
     P.price_in = x->use_comm ? x->recv : x->send;
     P.nin = G;
@@ -1445,6 +1446,7 @@ int spx_phase_times(spx_ctx* x, double out[SPX_PHASES]) {
     out[10] = h[19] * 0.01;  // update drain
     out[11] = h[22] * 0.01;  // price prologue
     out[12] = h[23] * 0.01;  // price drain
+    for (int k = 0; k < 5; ++k) out[13 + k] = h[24 + k] * 0.01;  // k_update workgroup 0 marks
     out[0] = h[1] * 0.01;  // 100 MHz ticks -> us
     out[1] = h[2] * 0.01;
     out[2] = h[5] * 0.01;

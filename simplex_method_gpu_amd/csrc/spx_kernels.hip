@@ -84,6 +84,11 @@ __device__ __forceinline__ void stamp_tail(unsigned long long* slot, unsigned lo
         __hip_atomic_store(&win[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
+// Workgroup 0 timeline of k_update (diagnostic): slot 24 + k accumulates
+// the ticks from its start to mark k (thread 0 only).
+__device__ __forceinline__ void wg0_mark(const Params& P, int k, unsigned long long t0) {
+    if (P.stamps && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.stamps[24 + k], rtime() - t0);
+}
 // Sub-phase marks inside the update tail: slot 8+k accumulates the ticks since
 // the previous mark (thread 0 only).
 __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, unsigned long long prev) {
@@ -751,12 +756,13 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
 // loads of B per lane per round trip.  a: A_p in global memory or in LDS.
 template <int U, int R>
 __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2* __restrict__ src, int64_t base,
-                                         int64_t L2, int lane, double (&acc)[R], const dbl2 (*pre)[R] = nullptr) {
+                                         int64_t L2, int lane, double (&acc)[R], const dbl2 (*pre)[R],
+                                         const dbl2 (&apre)[U], bool have_apre) {
     int64_t k = lane;
-    if (pre) {  // the first U chunks were loaded at kernel entry
+    if (pre) {  // the first U chunks were loaded at kernel entry (A_p's too when have_apre)
         dbl2 av[U];
 #pragma unroll
-        for (int t = 0; t < U; ++t) av[t] = a[k + t * 64];
+        for (int t = 0; t < U; ++t) av[t] = have_apre ? apre[t] : a[k + t * 64];
 #pragma unroll
         for (int t = 0; t < U; ++t) {
 #pragma unroll
@@ -810,14 +816,35 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // stream takes 23 us)
     // (the explicit in-place update measured slower with its old rows loaded
     // this way: C3 59 -> 66 us, so window only)
+    const unsigned long long t_wg0 = (P.stamps && blockIdx.x == 0) ? rtime() : 0ull;
     // the deferred pricing partials are loaded first: vmcnt retires in issue
     // order, so loads issued after the B prefetch would wait for all of it
     PricePartial pw0{INFINITY, INT64_MAX, 0.0, 0.0};
     if (P.defer_price && tid < P.price_grid) pw0 = P.price_partials[tid];
+    // the merged entering candidates (k_price's last workgroup, one record
+    // per rank: MINLOC, v4:294-302) likewise, and then A_p's first chunks:
+    // everything the stream's first fmas need is requested before the B
+    // prefetch floods the memory queues
+    double min_e0 = INFINITY;
+    int64_t p0 = INT64_MAX;
+    int gw0 = 0;
+    if (!P.defer_price) {
+        for (int g = 0; g < P.nin; ++g) {
+            const ArgMinEntry e = P.price_in[g * P.pr_stride];
+            if (argmin_better(e.val, e.idx, min_e0, p0)) { min_e0 = e.val; p0 = e.idx; gw0 = g; }
+        }
+    }
     constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
     const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    dbl2 apf[PFU];
+    const bool apf_ok = pf_ok && !P.defer_price && p0 >= 0 && p0 < P.n;
+    if (apf_ok) {
+        const dbl2* a0 = reinterpret_cast<const dbl2*>(P.A + p0 * P.L);
+#pragma unroll
+        for (int t = 0; t < PFU; ++t) apf[t] = a0[lane + t * 64];
+    }
     if (pf_ok) {
         const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + pf_row * (P.L >> 1);
 #pragma unroll
@@ -826,6 +853,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             for (int u = 0; u < R; ++u) pfb[t][u] = ld2<SPX_NT_BLOAD>(&b0[u * (P.L >> 1) + lane + t * 64]);
     }
     if (stopped(st)) return;
+    wg0_mark(P, 0, t_wg0);
     unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
     stamp_start(slot);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -861,11 +889,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         p = t.idx;
         e_enter = t.pad;
     } else {
-        for (int g = 0; g < P.nin; ++g) {
-            const ArgMinEntry e = P.price_in[g * P.pr_stride];
-            if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
-        }
+        min_e = min_e0;
+        p = p0;
+        gw = gw0;
     }
+    wg0_mark(P, 1, t_wg0);
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
@@ -932,6 +960,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
+    wg0_mark(P, 2, t_wg0);
     if constexpr (WIN) {
         // eta window: B_w is only read; alpha_i = B_w[i,:] . A_p +
         // sum_tau U[i][tau] Wt[p][tau], the window terms (lane tau) joining the
@@ -941,24 +970,16 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                                        : P.Wt + p * KW;
         const double wl = lane < nw ? wrec[lane] : 0.0;
         // s_x = r_tau . b = xw[q] + sum_{s<tau} U[q][s] Wt[n][s] (v4:347), also
-        // kept as Wt[n][tau] for later pivots and the fold
-        double sxw = 0.0;
+        // kept as Wt[n][tau] for later pivots and the fold: the operands are
+        // loaded here, the sum is formed after the stream (a dependent load +
+        // butterfly here delayed every wave's stream)
+        double sx_u = 0.0, sx_w = 0.0, sx_x = 0.0;
         if (pend) {
-            sxw = lane < tau ? P.U[qp * KW + lane] * P.Wt[P.n * KW + lane] : 0.0;
-            sxw = P.xw[qp] + wave_sum(sxw);
-            if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
-        }
-        if (pend && lane == 0) {
-            // the exact Wt entries of the basic columns for the pending pivot:
-            // r_tau . A_j = aq for its entering column, 0 for the others (their
-            // B^-1 A_j is a unit vector).  Issued before the stream so the
-            // stores retire under it.
-            const int64_t q = st->q;
-            const double aq = st->aq;
-            for (int u = 0; u < nvalid; ++u) {
-                const int64_t i = gr0 + u;
-                P.Wt[P.b_ixs[i] * KW + tau] = (i == q) ? aq : 0.0;
+            if (lane < tau) {
+                sx_u = P.U[qp * KW + lane];
+                sx_w = P.Wt[P.n * KW + lane];
             }
+            sx_x = P.xw[qp];
         }
         // A_p staged in LDS once per workgroup (SPX_WIN_APLDS) instead of
         // every wave re-reading it through L1/L2 beside the B stream
@@ -974,9 +995,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             static_assert(U == PFU, "prefetch and stream chunking agree");
             if (SPX_WIN_APLDS && aplds)
                 win_rows<U, R>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc,
-                               pf_ok ? pfb : nullptr);
+                               pf_ok ? pfb : nullptr, apf, false);
             else
-                win_rows<U, R>(ap, src, base, L2, lane, acc, pf_ok ? pfb : nullptr);
+                win_rows<U, R>(ap, src, base, L2, lane, acc, pf_ok ? pfb : nullptr, apf, apf_ok);
         } else if (nvalid > 0) {
             for (int64_t k = lane; k < L2; k += 64) {
                 const dbl2 av = ap[k];
@@ -994,6 +1015,20 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                 const double cu = lane < tau ? ucv[u] : (lane == tau ? ei[u] : 0.0);
                 acc[u] = fma(cu, wl, acc[u]);
                 if (pend && lane == 0) P.U[li * KW + tau] = ei[u];
+            }
+        }
+        double sxw = 0.0;
+        if (pend) {
+            sxw = sx_x + wave_sum(sx_u * sx_w);
+            if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
+            if (lane == 0) {
+                // the exact Wt entries of the basic columns for the pending
+                // pivot: r_tau . A_j = aq for its entering column, 0 for the
+                // others (their B^-1 A_j is a unit vector)
+                for (int u = 0; u < nvalid; ++u) {
+                    const int64_t i = gr0 + u;
+                    P.Wt[bixv[u] * KW + tau] = (i == qp) ? aqp : 0.0;
+                }
             }
         }
         if (upd_x) sxa = sxw;
@@ -1062,6 +1097,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     }
 
     stamp_stream(win, false);
+    wg0_mark(P, 3, t_wg0);
     const double s_x = (upd_x && nvalid > 0) ? (WIN ? sxa : wave_sum(sxa)) : 0.0;
 
     // x_b += s_x E (v4:348) for the owned rows; alpha_i, theta_i
@@ -1114,6 +1150,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             UpdPartial w = red[0];
             for (int i = 1; i < WAVES; ++i) upd_merge(w, red[i]);
             upd_publish_tagged(P, blockIdx.x, w, tag, lane);
+            wg0_mark(P, 4, t_wg0);
         }
         if (blockIdx.x != gridDim.x - 1) return;
         const unsigned long long t_tail = slot ? rtime() : 0;

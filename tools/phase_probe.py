@@ -20,4 +20,4 @@ for kw in json.loads(a.variants):
         ctx.phase_times()
         ctx.iterate(a.k)
         ph = ctx.phase_times()
-    print(json.dumps({"kw": kw, **{k: round(v / a.k, 2) for k, v in ph.items()}}), flush=True)
+    print(json.dumps({"kw": kw, **{k: (round(v / a.k, 2) if not isinstance(v, list) else [round(x / a.k, 2) for x in v]) for k, v in ph.items()}}), flush=True)
