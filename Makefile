@@ -62,28 +62,28 @@ variant:
 	  -DSPX_NT_BLOAD=$(word 2,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
 	  -DSPX_NT_BSTORE=$(word 3,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
 	  -c $(SRC)/spx_kernels.hip -o $(BUILD)/v$(NT)/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/v$(NT)/libsimplex.so $(BUILD)/v$(NT)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/v$(NT)/libsimplex.so $(BUILD)/v$(NT)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
 
 # in-place vs ping-pong B^-1 storage: make pingpong
 pingpong:
 	@mkdir -p $(BUILD)/pp
 	$(HIPCC) $(HIPFLAGS) -DSPX_INPLACE=0 -c $(SRC)/spx_kernels.hip -o $(BUILD)/pp/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/pp/libsimplex.so $(BUILD)/pp/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/pp/libsimplex.so $(BUILD)/pp/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
 
 # diagnostic (timing-only, wrong results): update kernel without its tail
 diag_notail:
 	@mkdir -p $(BUILD)/notail
 	$(HIPCC) $(HIPFLAGS) -DSPX_DIAG_SKIP_TAIL=1 -c $(SRC)/spx_kernels.hip -o $(BUILD)/notail/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/notail/libsimplex.so $(BUILD)/notail/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/notail/libsimplex.so $(BUILD)/notail/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
 
 # generic experiment build: make xlib X=name XFLAGS="-DSPX_WIN_APLDS=1"
 xlib:
 	@mkdir -p $(BUILD)/x$(X)
 	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_kernels.hip -o $(BUILD)/x$(X)/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/x$(X)/libsimplex.so $(BUILD)/x$(X)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/x$(X)/libsimplex.so $(BUILD)/x$(X)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
 
 # persistent-loop experiment build: make xloop X=name XFLAGS="-DSPX_LOOP_FU=4"
 xloop:
 	@mkdir -p $(BUILD)/l$(X)
 	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_loop.hip -o $(BUILD)/l$(X)/spx_loop.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/l$(X)/libsimplex.so $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/l$(X)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/l$(X)/libsimplex.so $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/l$(X)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)

@@ -28,7 +28,17 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 #ifndef SPX_NT_BSTORE
 #define SPX_NT_BSTORE 1 // update writes of B_new
 #endif
-
+// Eta-window FTRAN reads of the read-only base B_w (k_update): default policy
+// while B_w is at most SPX_BWIN_CACHED bytes, non-temporal beyond.  B_w is
+// rewritten by k_fold's default-policy stores and read back every pass between
+// A streams loaded non-temporally, so a B_w that fits the 256 MiB Infinity
+// Cache stays partly resident.  Measured (tools/policy_win.sh, r02_bwin.sh):
+// C3 (134 MB) k_update 31.8 us nt -> 28.0 us default; C5 (2.1 GB, two-kernel
+// passes) 352-360 us nt against 383-410 us default.
+#ifndef SPX_BWIN_CACHED
+#define SPX_BWIN_CACHED (192ll << 20)
+#endif
+__host__ __device__ inline bool win_b_cached(const Params& P) { return P.m * P.L * 8 <= SPX_BWIN_CACHED; }
 template <int NT>
 __device__ __forceinline__ dbl2 ld2(const dbl2* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);

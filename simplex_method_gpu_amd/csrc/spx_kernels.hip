@@ -754,7 +754,7 @@ __device__ void update_tail_rs(const Params& P, DevState* st, int64_t it, int pa
 
 // Eta-window FTRAN rows: acc[u] += B_w[row u,:] . A_p for R full rows, U dbl2
 // loads of B per lane per round trip.  a: A_p in global memory or in LDS.
-template <int U, int R>
+template <int U, int R, int BNT>
 __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2* __restrict__ src, int64_t base,
                                          int64_t L2, int lane, double (&acc)[R], const dbl2 (*pre)[R],
                                          const dbl2 (&apre)[U], bool have_apre) {
@@ -779,7 +779,7 @@ __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2*
         for (int t = 0; t < U; ++t) {
             av[t] = a[k + t * 64];
 #pragma unroll
-            for (int u = 0; u < R; ++u) bv[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
+            for (int u = 0; u < R; ++u) bv[t][u] = ld2<BNT>(&src[base + u * L2 + k + t * 64]);
         }
 #pragma unroll
         for (int t = 0; t < U; ++t) {
@@ -801,7 +801,7 @@ __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2*
     }
 }
 
-template <int BLOCK, int R, bool RS, bool WIN>
+template <int BLOCK, int R, bool RS, bool WIN, int BNT>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
     using Lds = UpdLds<BLOCK>;
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
         for (int t = 0; t < PFU; ++t)
 #pragma unroll
-            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<SPX_NT_BLOAD>(&b0[u * (P.L >> 1) + lane + t * 64]);
+            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * (P.L >> 1) + lane + t * 64]);
     }
     if (stopped(st)) return;
     wg0_mark(P, 0, t_wg0);
@@ -994,10 +994,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
             static_assert(U == PFU, "prefetch and stream chunking agree");
             if (SPX_WIN_APLDS && aplds)
-                win_rows<U, R>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc,
+                win_rows<U, R, BNT>(reinterpret_cast<const dbl2*>(smem + Lds::bytes), src, base, L2, lane, acc,
                                pf_ok ? pfb : nullptr, apf, false);
             else
-                win_rows<U, R>(ap, src, base, L2, lane, acc, pf_ok ? pfb : nullptr, apf, apf_ok);
+                win_rows<U, R, BNT>(ap, src, base, L2, lane, acc, pf_ok ? pfb : nullptr, apf, apf_ok);
         } else if (nvalid > 0) {
             for (int64_t k = lane; k < L2; k += 64) {
                 const dbl2 av = ap[k];
@@ -1773,14 +1773,14 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
     return hipErrorInvalidValue;
 }
 
-template <int BLOCK, int R, bool RS, bool WIN>
+template <int BLOCK, int R, bool RS, bool WIN, int BNT = 1>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = UpdLds<BLOCK>::bytes + ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0);
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
+        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
                               P);
     } else {
-        hipLaunchKernelGGL((k_update<BLOCK, R, RS, WIN>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
     return hipGetLastError();
 }
@@ -1788,8 +1788,11 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
 template <int BLOCK, int R>
 static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (P.row_shard) return launch_update_k<BLOCK, R, true, false>(P, grid, s, e0, e1);
-    return P.win ? launch_update_k<BLOCK, R, false, true>(P, grid, s, e0, e1)
-                 : launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
+    if (!P.win) return launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
+    // B_w loads: default policy while B_w fits the Infinity Cache beside the
+    // window state (spx_common.h SPX_NT_BWIN), non-temporal beyond
+    if (win_b_cached(P)) return launch_update_k<BLOCK, R, false, true, 0>(P, grid, s, e0, e1);
+    return launch_update_k<BLOCK, R, false, true, 1>(P, grid, s, e0, e1);
 }
 
 hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
