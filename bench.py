@@ -7,9 +7,10 @@ MINLOC, FTRAN, ratio test, B^-1 update, x_b / y update) on the seeded dense
 random LP of SURVEY.md §8(d) (default C3: m=4096, n=16384, fp64), with A, b, c
 generated directly in HBM.
 
-B^-1 is kept as an eta window of 64 (B_w + U R) at every N: its
-rank-63 fold runs every 63 pivots, so the timed region is aligned to whole
-windows — W untimed warm-up pivots, then untimed pivots up to the next window
+B^-1 is kept in the representation the library picks for (m, n) — the eta
+window of 64 (B_w + U R) at m >= 2048 (C3, C4, C5), the explicit
+inverse at C2 — at every N.  The window's rank-63 fold runs every 63 pivots, so
+the timed region is aligned to whole windows — W untimed warm-up pivots, then untimed pivots up to the next window
 boundary, then K rounded up to a multiple of 63 timed pivots, which therefore
 hold exactly K/63 folds (`timed_region` reports the pivots, folds and hipGraph
 replays the library enqueued there, and `config.dispatch` is derived from
@@ -19,8 +20,8 @@ the same clock.
 
 Multi-GPU (torch.distributed.run, one process per GPU): the north-star
 partitioning — pricing columns sharded over the ranks with an RCCL all-gather
-MINLOC per iteration, B^-1 (eta window 64) replicated, so N=1 runs the same
-representation as N>1.  `--row-shard` instead row-shards an explicit B^-1
+MINLOC per iteration, B^-1 replicated, so N=1 runs the same representation as
+N>1.  `--row-shard` instead row-shards an explicit B^-1
 (SURVEY.md §8f row 1).  The job does one iteration per step on a fixed LP
 ("strong" scaling); `pricing` reports the aggregate pricing throughput (all
 ranks' algorithmic pricing bytes / max-over-ranks of pricing kernel + MINLOC
@@ -47,8 +48,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CONFIGS = {"C2": (1024, 4096), "C3": (4096, 16384), "C4": (4096, 131072), "C5": (16384, 65536)}
-METRIC = "simplex iterations/sec on dense m=4096 n=16384 fp64; achieved HBM GB/s"
-DEFAULT_WINDOW = 64
+METRIC = "simplex iterations/sec on dense m={m} n={n} fp64; achieved HBM GB/s"  # BASELINE.json at C3
 
 
 def parse():
@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--price-block", type=int, default=0)
     ap.add_argument("--graph-batch", type=int, default=0)
     ap.add_argument("--window", type=int, default=0,
-                    help="B^-1 representation: 0 = eta window 64 (explicit with --row-shard), "
+                    help="B^-1 representation: 0 = the library's choice (eta window 64 at m >= 2048, "
+                         "explicit below and with --row-shard), "
                          "-1 explicit rank-1 update, 8/16/32/64 eta window")
     ap.add_argument("--row-shard", action="store_true",
                     help="N > 1: row-shard an explicit B^-1 over the ranks (SURVEY.md §8f row 1) "
@@ -85,7 +86,7 @@ def parse():
     a.m = a.m or m
     a.n = a.n or n
     if a.window == 0:
-        a.window = -1 if a.row_shard else DEFAULT_WINDOW
+        a.window = -1 if a.row_shard else 0
     return a
 
 
@@ -261,7 +262,7 @@ def main():
         rep = ("eta window %d: B_w + U R, FTRAN stream read-only, rank-%d fold every %d pivots" % (win, win - 1, win - 1)
                if win else "explicit B^-1, rank-1 update in place every pivot (v4:331-333)")
         out = {
-            "metric": METRIC,
+            "metric": METRIC.format(m=m, n=n),
             "value": value,
             "unit": "iterations/s",
             "n_gpus": world,

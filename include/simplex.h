@@ -75,7 +75,8 @@ typedef struct spx_opts {
     int32_t price_grid;   /* tuning: pricing workgroups, 0 = auto              */
     int32_t flags;        /* SPX_FLAG_* bits                                   */
     int32_t update_block; /* tuning: threads per update workgroup, 0 = auto    */
-    int32_t window;       /* B^-1 representation: 0 = auto,
+    int32_t window;       /* B^-1 representation: 0 = auto
+                             (window 64 at m >= 2048, else explicit),
                              -1 = explicit B^-1 rewritten by a rank-1 update
                              every pivot (v4:331-333), 8/16/32/64 = eta window:
                              B^-1 = B_w + U R kept for up to window-1 pivots,

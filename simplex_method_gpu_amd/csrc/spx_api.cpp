@@ -306,10 +306,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     int KW = x->opts.window;
     if (KW == 0) {
         // auto (measured): the window halves the B^-1 stream and
-        // costs ~5 % more pricing, so it pays once m^2 is not small against
-        // m (n - m): C3 +19 %, C5 +28 %; C4 (n = 32 m) and C2 (m = 1024,
-        // latency-bound) stay explicit.  Row-sharded B^-1 is always explicit.
-        const bool pays = m >= 2048 && (double)m >= 0.06 * (double)(n - m);
+        // costs ~2 % more pricing (its Wt rows): C3 +27 %, C4 +4 %, C5 +33 %
+        // against the explicit update; C2 (m = 1024, latency-bound: 45.8k vs
+        // 52.1k it/s) stays explicit.  Row-sharded B^-1 is always explicit.
+        const bool pays = m >= 2048;
         KW = (pays && !P.row_shard) ? 64 : -1;
     }
     // Devex pricing takes the pivot row from the eta-window pricing pass

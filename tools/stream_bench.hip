@@ -21,7 +21,7 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
     } while (0)
 
 // one wave per row (R rows per wave), U dbl2 loads per lane per round trip
-template <int U, int R>
+template <int U, int R, int NT = 1>
 __global__ __launch_bounds__(512) void k_rows(const double* __restrict__ B, const double* __restrict__ a,
                                               double* __restrict__ out, long rows, long L) {
     const int lane = threadIdx.x & 63;
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(512) void k_rows(const double* __restrict__ B, cons
             dbl2 bv[U], av[U];
 #pragma unroll
             for (int t = 0; t < U; ++t) {
-                bv[t] = __builtin_nontemporal_load(&src[k + t * 64]);
+                bv[t] = NT ? __builtin_nontemporal_load(&src[k + t * 64]) : src[k + t * 64];
                 av[t] = ap[k + t * 64];
             }
 #pragma unroll
@@ -125,6 +125,29 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(k_flat, dim3(1024), dim3(512), 0, 0, B, out, (long)(bytes / 16));
     };
     report("flat grid-stride, cold", timeit(flat, reps) - tf);
+    // default-policy rows: Infinity Cache residency of B between launches,
+    // alone and behind a 3x-sized non-temporal stream (the pricing pass's A)
+    auto rows8d = [&]() { hipLaunchKernelGGL((k_rows<8, 1, 0>), dim3((rows + 7) / 8), dim3(512), 0, 0, B, a, out, rows, L); };
+    report("rows U8 R1 default policy, back-to-back", timeit(rows8d, reps));
+    auto rows8dc = [&]() {
+        flushk();
+        hipLaunchKernelGGL((k_rows<8, 1, 0>), dim3((rows + 7) / 8), dim3(512), 0, 0, B, a, out, rows, L);
+    };
+    report("rows U8 R1 default policy, cold", timeit(rows8dc, reps) - tf);
+    const long an2 = (long)(3 * bytes / 16);
+    auto astream = [&]() { hipLaunchKernelGGL(k_flat, dim3(2048), dim3(512), 0, 0, flush, out, an2); };
+    const float ta = timeit(astream, reps);
+    auto rows8da = [&]() {
+        astream();
+        hipLaunchKernelGGL((k_rows<8, 1, 0>), dim3((rows + 7) / 8), dim3(512), 0, 0, B, a, out, rows, L);
+    };
+    report("rows U8 R1 default policy, behind a 3x nt stream", timeit(rows8da, reps) - ta);
+    auto rows8na = [&]() {
+        astream();
+        hipLaunchKernelGGL((k_rows<8, 1, 1>), dim3((rows + 7) / 8), dim3(512), 0, 0, B, a, out, rows, L);
+    };
+    report("rows U8 R1 nt, behind a 3x nt stream", timeit(rows8na, reps) - ta);
+    std::printf("{\"kernel\": \"3x nt stream\", \"us\": %.2f}\n", ta);
     std::printf("{\"kernel\": \"flush 1GiB\", \"us\": %.2f}\n", tf);
     return 0;
 }
