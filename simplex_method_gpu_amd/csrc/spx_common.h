@@ -179,6 +179,22 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 __device__ __forceinline__ bool stopped(const DevState* st) {
     return st->status != ST_RUNNING || st->iter >= st->limit;
 }
+__device__ __forceinline__ bool stopped(const DevState& s) { return s.status != ST_RUNNING || s.iter >= s.limit; }
+// The loop state in one memory round trip: DevState as independent 16-byte
+// loads issued together.  (The kernels also store to *st, so the compiler
+// cannot use scalar loads, and field-by-field reads became a chain of
+// dependent vector round trips at kernel entry.)
+__device__ __forceinline__ DevState st_snapshot(const DevState* st) {
+    static_assert(sizeof(DevState) % 16 == 0, "DevState is a whole number of 16-byte words");
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    struct Words {
+        u32x4 w[sizeof(DevState) / 16];
+    } v;
+    const u32x4* p = reinterpret_cast<const u32x4*>(st);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(DevState) / 16); ++i) v.w[i] = p[i];
+    return __builtin_bit_cast(DevState, v);
+}
 
 __device__ __forceinline__ unsigned long long rtime() { return __builtin_amdgcn_s_memrealtime(); }
 

@@ -122,7 +122,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // speculative: this wave's first non-basic column, loaded together with the
     // status word (index clamped into the list; validated against nb_count)
     const int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
-    if (stopped(st)) return;
+    const DevState S = st_snapshot(st);
+    if (stopped(S)) return;
     unsigned long long* const slot = P.stamps;
     stamp_start(slot);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -133,23 +134,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     PricePartial* red =
         reinterpret_cast<PricePartial*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0));
     int* s_last = reinterpret_cast<int*>(red + WAVES);
-    const int nb = st->nb_count;
+    const int nb = S.nb_count;
 
-    // the first CH chunks of the first column stay in flight during the y
-    // staging below (the A stream does not wait for the LDS fill)
-    constexpr int CH = 8;
-    const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
-    dbl2 v0[CH];
-    if (pre) {
-        const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
-#pragma unroll
-        for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&c0[lane + u * 64]);
-    }
-
-    const int64_t it = st->iter;
+    const int64_t it = S.iter;
     const bool wg0 = blockIdx.x == 0;
     constexpr int YB = 4;
-    const dbl2* yin = reinterpret_cast<const dbl2*>(st->y_buf ? P.y1 : P.y0);
+    const dbl2* yin = reinterpret_cast<const dbl2*>(S.y_buf ? P.y1 : P.y0);
     // explicit B^-1: current y = ybuf + s_y r while the last pivot's y update is
     // pending (workgroup 0 also persists that y and, in place, stages r for
     // k_update).  Eta window: y_w is fixed between folds; the pending pivot's
@@ -157,35 +147,77 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // U[q][s<tau], in Qrows/Urows for k_fold).  Loads are batched YB deep per
     // thread so the fill is one memory round trip, not one per element.
     const int KW = P.win;
-    const int nw = WIN ? st->nw : 0;
+    const int nw = WIN ? S.nw : 0;
     if (WIN && nw >= KW) {  // the host folds before this can happen
         if (wg0 && tid == 0) st->status = ST_WINDOW_FULL;
         return;
     }
     const bool pend = WIN ? nw > 0 : it > 0;
     const int tau = nw - 1;  // pending pivot of the window
-    const bool upd_y = !WIN && st->y_applied < it;
-    const double s_y = st->s_y;
-    dbl2* yout = reinterpret_cast<dbl2*>(st->y_buf ? P.y0 : P.y1);
+    const int64_t qq = pend ? S.q : 0;
+    const bool upd_y = !WIN && S.y_applied < it;
+    const double s_y = S.s_y;
+    dbl2* yout = reinterpret_cast<dbl2*>(S.y_buf ? P.y0 : P.y1);
     // the pending pivot row: row q of the stored B^-1 (replicated storage), or
     // rbuf, staged by k_finalize_rs from the all-gather (row-sharded storage)
     const dbl2* rr = reinterpret_cast<const dbl2*>(
         !pend ? P.zeros
-              : (P.row_shard ? P.rbuf : ((SPX_INPLACE || WIN || !(it & 1)) ? P.B0 : P.B1) + st->q * L));
+              : (P.row_shard ? P.rbuf : ((SPX_INPLACE || WIN || !(it & 1)) ? P.B0 : P.B1) + qq * L));
     const bool stage_r = WIN ? (pend && wg0) : (SPX_INPLACE && pend && wg0 && !P.row_shard);
-    if (LDS_Y || LDS_R || wg0) {
+    const bool stage = LDS_Y || LDS_R || wg0;
+    const bool load_y = LDS_Y || (!WIN && wg0);
+    const bool need_r = WIN ? (pend && (LDS_R || stage_r)) : (upd_y || stage_r);
+
+    // Issue order (vmcnt retires in issue order): the first batch of y /
+    // base-row loads, then the first CH chunks of this wave's first column,
+    // which stay in flight across the LDS fill and the barrier.  Every load
+    // here is unconditional with a clamped index (rr is always a valid row),
+    // so the fill waits for its own loads only, not for the A prefetch.
+    constexpr int CH = 8;
+    const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
+    dbl2 yv[YB], rv[YB];
+    double uqrow = 0.0;  // U[q][tid] for Urows (window, workgroup 0)
+    if (stage) {
+#pragma unroll
+        for (int u = 0; u < YB; ++u) {
+            const int64_t k = (int64_t)u * BLOCK + tid;
+            const int64_t kc = k < L2 ? k : L2 - 1;
+            if (load_y) yv[u] = yin[kc];
+            rv[u] = rr[kc];
+        }
+        if constexpr (WIN) uqrow = P.U[qq * KW + (tid < KW ? tid : KW - 1)];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would hoist the A loads)
+    dbl2 v0[CH];
+    if constexpr (WM != 3) {
+        const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t k = lane + u * 64;
+            v0[u] = ld2<SPX_NT_A>(&c0[k < L2 ? k : L2 - 1]);
+        }
+    }
+    if (stage) {
+        // the staging values are taken here, behind the A prefetch's issue
+        // (otherwise the loads sink into the conditional stores below and
+        // their waits cover the prefetch too)
+#pragma unroll
+        for (int u = 0; u < YB; ++u) {
+            if (load_y) asm volatile("" ::"v"(yv[u].x), "v"(yv[u].y));
+            asm volatile("" ::"v"(rv[u].x), "v"(rv[u].y));
+        }
+        if constexpr (WIN) asm volatile("" ::"v"(uqrow));
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
         dbl2* rl = reinterpret_cast<dbl2*>(rs);
         dbl2* rb = reinterpret_cast<dbl2*>(WIN ? P.Qrows + (int64_t)tau * L : P.rbuf);
-        const bool need_r = WIN ? (pend && (LDS_R || stage_r)) : (upd_y || stage_r);
         for (int64_t k0 = 0; k0 < L2; k0 += (int64_t)YB * BLOCK) {
-            dbl2 yv[YB], rv[YB];
+            if (k0 > 0) {  // later batches (L2 > YB * BLOCK)
 #pragma unroll
-            for (int u = 0; u < YB; ++u) {
-                const int64_t k = k0 + (int64_t)u * BLOCK + tid;
-                if (k < L2) {
-                    if (LDS_Y || (!WIN && wg0)) yv[u] = yin[k];
-                    if (need_r) rv[u] = rr[k];
+                for (int u = 0; u < YB; ++u) {
+                    const int64_t k = k0 + (int64_t)u * BLOCK + tid;
+                    const int64_t kc = k < L2 ? k : L2 - 1;
+                    if (load_y) yv[u] = yin[kc];
+                    if (need_r) rv[u] = rr[kc];
                 }
             }
 #pragma unroll
@@ -206,9 +238,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 }
             }
         }
-        if (WIN && stage_r && tid < tau) P.Urows[(int64_t)tau * KW + tid] = P.U[st->q * KW + tid];
+        if (WIN && stage_r && tid < tau) P.Urows[(int64_t)tau * KW + tid] = uqrow;
     }
-    if constexpr (LDS_Y || LDS_R) __syncthreads();
+    // LDS only: the A prefetch stays in flight across the barrier (the staged
+    // Qrows / rbuf stores are read after the kernel boundary)
+    if constexpr (LDS_Y || LDS_R) lds_barrier();
     auto Y = [&](int64_t k) -> dbl2 {
         if constexpr (LDS_Y) return reinterpret_cast<const dbl2*>(ys)[k];
         else if constexpr (WIN) return yin[k];
@@ -223,7 +257,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if constexpr (WIN) {
         if (pend) {
             if (lane < tau) {
-                uq = P.U[st->q * KW + lane];
+                uq = P.U[qq * KW + lane];
                 syl = P.SY[lane];
             }
             syp = P.SY[tau];
@@ -232,8 +266,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 
     double best = INFINITY, bw = 0.0, be = 0.0;
     int64_t bj = INT64_MAX;
-    const int64_t dvx_leave = st->leave;
-    const double dvx_wp = st->wp, dvx_aq = st->aq;
+    const int64_t dvx_leave = S.leave;
+    const double dvx_wp = S.wp, dvx_aq = S.aq;
     unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
     const int nlist = nb;
@@ -264,10 +298,9 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         __shared__ double s_sy[64], s_uq[64];
         if (tid < 64) {
             s_sy[tid] = (pend && tid <= tau) ? P.SY[tid] : 0.0;
-            s_uq[tid] = (pend && tid < tau) ? P.U[st->q * KW + tid] : 0.0;
+            s_uq[tid] = (pend && tid < tau) ? P.U[qq * KW + tid] : 0.0;
         }
         __syncthreads();
-        const int64_t qq = pend ? st->q : 0;
         for (int base = (blockIdx.x * WAVES + wave) * 64; base < nlist; base += stride * 64) {
             const int idx = base + lane;
             const bool cv = idx < nlist;
@@ -659,12 +692,12 @@ __device__ __forceinline__ void tail_last(const Params& P, TailPre* t) {
     if (t && t->valid && t->kp >= 0) t->last = P.nb_list[t->cnt - 1];
 }
 
-__device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState* st, int64_t p) {
+__device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState& S, int64_t p) {
     TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
     if (p < 0 || p >= P.n) return t;
-    if (P.win) t.nw = st->nw;
+    if (P.win) t.nw = S.nw;
     t.c_p = P.c[p];
-    t.cnt = st->nb_count;
+    t.cnt = S.nb_count;
     if (owns_col(P, p)) t.kp = P.nb_pos[p];  // (nb_list[cnt - 1] is loaded by the tail: tail_last)
     if (P.devex) t.wp = P.W[p];
     t.valid = true;
@@ -821,6 +854,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // order, so loads issued after the B prefetch would wait for all of it
     PricePartial pw0{INFINITY, INT64_MAX, 0.0, 0.0};
     if (P.defer_price && tid < P.price_grid) pw0 = P.price_partials[tid];
+    const DevState Sv = st_snapshot(st);  // the loop state in one round trip
     // the merged entering candidates (k_price's last workgroup, one record
     // per rank: MINLOC, v4:294-302) likewise, and then A_p's first chunks:
     // everything the stream's first fmas need is requested before the B
@@ -852,7 +886,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
             for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * (P.L >> 1) + lane + t * 64]);
     }
-    if (stopped(st)) return;
+    if (stopped(Sv)) return;
     wg0_mark(P, 0, t_wg0);
     unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
     stamp_start(slot);
@@ -903,7 +937,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         return;
     }
 
-    const int64_t it = st->iter;
+    const int64_t it = Sv.iter;
     const int par = (int)(it & 1);
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
     // row-sharded storage always ping-pongs (its tail recomputes the winner
@@ -915,15 +949,15 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     const double* a_prev = par ? P.alpha1 : P.alpha0;  // alpha of pivot it-1
     double* a_new = par ? P.alpha0 : P.alpha1;
     // the pending pivot it-1: r = S[q,:], E from a_prev and aq
-    const int nw = WIN ? st->nw : 0;
+    const int nw = WIN ? Sv.nw : 0;
     const int tau = nw - 1;  // eta window: the pending pivot
     const bool pend = WIN ? nw > 0 : it > 0;
-    const int64_t qp = st->q;
-    const double aqp = st->aq;
+    const int64_t qp = Sv.q;
+    const double aqp = Sv.aq;
     const double* rrow = !pend ? P.zeros : ((SPX_INPLACE || RS) ? P.rbuf : S + qp * L);
     const dbl2* __restrict__ rp = reinterpret_cast<const dbl2*>(rrow);
     const dbl2* __restrict__ ap = reinterpret_cast<const dbl2*>(P.A + p * L);
-    const bool upd_x = st->xb_applied < it;
+    const bool upd_x = Sv.xb_applied < it;
 
     // s_x = r.b (v4:347) for the deferred x_b update is accumulated inside the
     // row stream (every wave streams all of r; lane-strided, k ascending, then
@@ -952,7 +986,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     for (int u = 0; u < R; ++u)
         ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
     TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
-    if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st, p);
+    if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv, p);
     if (P.defer_price) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
@@ -1247,7 +1281,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
     }
     const double s_x = upd_x ? sxw : 0.0;
     TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
-    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st, p);
+    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st_snapshot(st), p);
     if (P.defer_price) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
