@@ -717,7 +717,7 @@ int iterate(spx_ctx* x, int64_t k) {
     return SPX_OK;
 }
 
-// Persistent loop: one cooperative launch per window (k_loop), folds between.
+// Persistent loop: one launch per window (k_loop, co-resident grid), folds between.
 int iterate_persist(spx_ctx* x, int64_t k) {
     int64_t left = k;
     while (left > 0) {

@@ -12,7 +12,7 @@
 //   dw  += SY Wt^T
 // which moves 16 L n bytes per window instead of 8(m+1)(n-m) + 8m^2 per pivot.
 // k_tab_build rebuilds T_w = B_w A after a reinversion or a warm start;
-// k_tab_loop runs whole passes in one cooperative launch.
+// k_tab_loop runs whole passes in one launch of a co-resident grid.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_tab_build(Params P) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent tableau loop: whole passes in ONE cooperative launch, two grid
+// Persistent tableau loop: whole passes in ONE launch (co-resident grid), two grid
 // barriers per pass, as k_loop (spx_loop.h) does for the eta window.  A
 // tableau pass moves a few MB, so what it pays for is dependent round trips
 // and barriers; the loop runs on few workgroups (cheap barriers: 1.3 us at
