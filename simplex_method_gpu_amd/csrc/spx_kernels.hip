@@ -263,7 +263,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             syp = P.SY[tau];
         }
     }
-
     double best = INFINITY, bw = 0.0, be = 0.0;
     int64_t bj = INT64_MAX;
     const int64_t dvx_leave = S.leave;
@@ -692,12 +691,12 @@ __device__ __forceinline__ void tail_last(const Params& P, TailPre* t) {
     if (t && t->valid && t->kp >= 0) t->last = P.nb_list[t->cnt - 1];
 }
 
-__device__ __forceinline__ TailPre tail_prefetch(const Params& P, const DevState& S, int64_t p) {
+__device__ __forceinline__ TailPre tail_prefetch(const Params& P, int32_t nw, int32_t cnt, int64_t p) {
     TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
     if (p < 0 || p >= P.n) return t;
-    if (P.win) t.nw = S.nw;
+    if (P.win) t.nw = nw;
     t.c_p = P.c[p];
-    t.cnt = S.nb_count;
+    t.cnt = cnt;
     if (owns_col(P, p)) t.kp = P.nb_pos[p];  // (nb_list[cnt - 1] is loaded by the tail: tail_last)
     if (P.devex) t.wp = P.W[p];
     t.valid = true;
@@ -849,16 +848,52 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     // stream takes 23 us)
     // (the explicit in-place update measured slower with its old rows loaded
     // this way: C3 59 -> 66 us, so window only)
+    // Issue order (vmcnt retires in issue order): the deferred pricing
+    // partials, then this wave's first B_w chunks -- unconditional with
+    // clamped indices, so the waits below count exactly and the price
+    // reduction does not wait for the B prefetch -- then the loop state,
+    // field by field (scalar loads: still in the entry block, after no store;
+    // a whole-struct snapshot's dead registers were reused at once, and as
+    // vector loads the uniform values were moved to scalar registers at once,
+    // both waits that held the prefetch), then the multi-rank candidate
+    // records and A_p's first chunks.  The status check comes after the price
+    // reduction; no store precedes it.
+    const int pgi = tid < P.price_grid ? tid : P.price_grid - 1;
+    const PricePartial pwl = P.price_partials[pgi];
+    constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
+    dbl2 pfb[PFU][R];
+    const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
+    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    if constexpr (WIN && !RS) {
+        const int64_t L2c = P.L >> 1;
+        const int64_t prow = pf_row + R <= P.m ? pf_row : (P.m >= R ? P.m - R : 0);
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + prow * L2c;
+#pragma unroll
+        for (int t = 0; t < PFU; ++t) {
+            const int64_t k = lane + t * 64 < L2c ? lane + t * 64 : L2c - 1;
+#pragma unroll
+            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * L2c + k]);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    struct {
+        int32_t status, nb_count, nw;
+        int64_t iter, limit, q, xb_applied;
+        double aq;
+    } Sv;
+    Sv.status = st->status;
+    Sv.nb_count = st->nb_count;
+    Sv.iter = st->iter;
+    Sv.limit = st->limit;
+    Sv.q = st->q;
+    Sv.aq = st->aq;
+    Sv.xb_applied = st->xb_applied;
+    Sv.nw = st->nw;
     const unsigned long long t_wg0 = (P.stamps && blockIdx.x == 0) ? rtime() : 0ull;
-    // the deferred pricing partials are loaded first: vmcnt retires in issue
-    // order, so loads issued after the B prefetch would wait for all of it
     PricePartial pw0{INFINITY, INT64_MAX, 0.0, 0.0};
-    if (P.defer_price && tid < P.price_grid) pw0 = P.price_partials[tid];
-    const DevState Sv = st_snapshot(st);  // the loop state in one round trip
+    if (P.defer_price && tid < P.price_grid) pw0 = pwl;
     // the merged entering candidates (k_price's last workgroup, one record
-    // per rank: MINLOC, v4:294-302) likewise, and then A_p's first chunks:
-    // everything the stream's first fmas need is requested before the B
-    // prefetch floods the memory queues
+    // per rank: MINLOC, v4:294-302), and then A_p's first chunks
     double min_e0 = INFINITY;
     int64_t p0 = INT64_MAX;
     int gw0 = 0;
@@ -868,10 +903,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             if (argmin_better(e.val, e.idx, min_e0, p0)) { min_e0 = e.val; p0 = e.idx; gw0 = g; }
         }
     }
-    constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
-    dbl2 pfb[PFU][R];
-    const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
-    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
     dbl2 apf[PFU];
     const bool apf_ok = pf_ok && !P.defer_price && p0 >= 0 && p0 < P.n;
     if (apf_ok) {
@@ -879,17 +910,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
         for (int t = 0; t < PFU; ++t) apf[t] = a0[lane + t * 64];
     }
-    if (pf_ok) {
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + pf_row * (P.L >> 1);
-#pragma unroll
-        for (int t = 0; t < PFU; ++t)
-#pragma unroll
-            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * (P.L >> 1) + lane + t * 64]);
-    }
-    if (stopped(Sv)) return;
-    wg0_mark(P, 0, t_wg0);
-    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
-    stamp_start(slot);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     // entering column: MINLOC over all ranks' candidates (v4:294-302), or,
@@ -927,6 +947,10 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         p = p0;
         gw = gw0;
     }
+    if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) return;
+    wg0_mark(P, 0, t_wg0);
+    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
+    stamp_start(slot);
     wg0_mark(P, 1, t_wg0);
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
@@ -985,8 +1009,8 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
     for (int u = 0; u < R; ++u)
         ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
-    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
-    if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv, p);
+    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
+    if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
     if (P.defer_price) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
@@ -1281,7 +1305,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
     }
     const double s_x = upd_x ? sxw : 0.0;
     TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
-    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st_snapshot(st), p);
+    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st->nw, st->nb_count, p);
     if (P.defer_price) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
