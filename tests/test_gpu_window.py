@@ -192,3 +192,12 @@ def test_window_large_invariants(spx, oracle, m, n, k, window):
     assert _rel(s["binv"] @ b, s["x_b"]) < 1e-10
     assert abs(z - float(c[s["b_ixs"]] @ s["x_b"])) <= 1e-10 * abs(z)
     assert np.all(s["x_b"] > -1e-9)
+
+
+@pytest.mark.parametrize("m,n,want", [(1024, 4096, 0), (2047, 4096, 0), (2048, 4096, 64), (4096, 16384, 64),
+                                      (4096, 131072, 64)])
+def test_auto_representation(spx, m, n, want):
+    """window = 0 picks the eta window of 64 at m >= 2048 (C3, C4, C5) and the
+    explicit rank-1 update below (C2); row-sharded B^-1 is always explicit."""
+    with spx.Context(m=m, n=n, seed=0) as ctx:
+        assert ctx.config()["window"] == want
