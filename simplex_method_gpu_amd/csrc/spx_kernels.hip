@@ -671,6 +671,17 @@ struct UpdLds {
     static constexpr size_t bytes = last + 16;
 };
 
+// Explicit in-place update (v4:331-333): the pivot row r, A_p and b are
+// staged in LDS once per workgroup (read from L2 per element they were three
+// operand streams beside the B stream), and each wave loads its next chunk of
+// B rows before storing this one (vmcnt counts stores too, so loads issued
+// behind a chunk's stores could not be waited for without them).  Needs the
+// three vectors in LDS and whole 4-chunk steps; from L = 2048 (C3 8.16k ->
+// 8.59k it/s, k_update 56 -> 47 us; at C2, L = 1024, the fill cost 1 %).
+__host__ __device__ inline bool upd_xlds(const Params& P) {
+    return !P.win && !P.row_shard && P.L >= 2048 && P.L * 24 <= 96 * 1024 && ((P.L >> 1) % 256) == 0;
+}
+
 // Basis bookkeeping (v4:339-342) + non-basic list swap-remove / append and
 // the deferred pivot state (spx_device.h).  One thread.
 // Scalars of the bookkeeping that only depend on the entering column, loaded
@@ -1019,6 +1030,24 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
     wg0_mark(P, 2, t_wg0);
+    // explicit update with r / A_p / b in LDS (upd_xlds): the whole workgroup
+    // stages them (every wave, whatever its rows)
+    const bool xl = !WIN && !RS && INPL && upd_xlds(P);
+    const dbl2* xr = reinterpret_cast<const dbl2*>(smem + Lds::bytes);
+    const dbl2* xa = xr + L2;
+    const dbl2* xb = xa + L2;
+    if constexpr (!WIN && !RS) {
+        if (xl) {
+            dbl2* d = reinterpret_cast<dbl2*>(smem + Lds::bytes);
+            for (int64_t kk = tid; kk < L2; kk += BLOCK) {
+                const dbl2 r2 = rp[kk], a2 = ap[kk], b2 = bp[kk];
+                d[kk] = r2;
+                d[L2 + kk] = a2;
+                d[2 * L2 + kk] = b2;
+            }
+            lds_barrier();
+        }
+    }
     if constexpr (WIN) {
         // eta window: B_w is only read; alpha_i = B_w[i,:] . A_p +
         // sum_tau U[i][tau] Wt[p][tau], the window terms (lane tau) joining the
@@ -1090,6 +1119,50 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             }
         }
         if (upd_x) sxa = sxw;
+    } else if (xl && nvalid == R) {
+        // r / A_p / b from LDS, B rows one 4-chunk step ahead (upd_xlds)
+        constexpr int U = (R >= 4) ? 2 : 4;
+        const int nit = (int)(L2 / (U * 64));
+        dbl2 bc[U][R], bn[U][R];
+        int64_t k = lane;
+#pragma unroll
+        for (int t = 0; t < U; ++t)
+#pragma unroll
+            for (int u = 0; u < R; ++u) bc[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + k + t * 64]);
+        for (int itn = 0; itn < nit; ++itn, k += U * 64) {
+            // the next step's rows (the first step's again on the last one:
+            // an unconditional load keeps the waits exact)
+            const int64_t kn = (itn + 1 < nit) ? k + U * 64 : (int64_t)lane;
+#pragma unroll
+            for (int t = 0; t < U; ++t)
+#pragma unroll
+                for (int u = 0; u < R; ++u) bn[t][u] = ld2<SPX_NT_BLOAD>(&src[base + u * L2 + kn + t * 64]);
+            dbl2 rv[U], av[U], bb[U];
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                rv[t] = xr[k + t * 64];
+                av[t] = xa[k + t * 64];
+                bb[t] = xb[k + t * 64];
+            }
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                sxa = fma(rv[t].x, bb[t].x, sxa);
+                sxa = fma(rv[t].y, bb[t].y, sxa);
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    dbl2 nv;
+                    nv.x = fma(ei[u], rv[t].x, bc[t][u].x);
+                    nv.y = fma(ei[u], rv[t].y, bc[t][u].y);
+                    st2<SPX_NT_BSTORE>(nv, &dst[base + u * L2 + k + t * 64]);
+                    acc[u] = fma(nv.x, av[t].x, acc[u]);
+                    acc[u] = fma(nv.y, av[t].y, acc[u]);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < U; ++t)
+#pragma unroll
+                for (int u = 0; u < R; ++u) bc[t][u] = bn[t][u];
+        }
     } else if (nvalid == R) {
         constexpr int U = (R >= 4) ? 2 : 4;
         static_assert(WIN || U == PFU, "prefetch and stream chunking agree");
@@ -1833,7 +1906,17 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
 
 template <int BLOCK, int R, bool RS, bool WIN, int BNT = 1>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const size_t lds = UpdLds<BLOCK>::bytes + ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0);
+    const size_t lds = UpdLds<BLOCK>::bytes + ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0) +
+                       ((!WIN && !RS && upd_xlds(P)) ? (size_t)P.L * 24 : 0);
+    if (lds > 65536) {  // once per instantiation (idempotent; not a stream operation)
+        static bool raised = false;
+        if (!raised) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_update<BLOCK, R, RS, WIN, BNT>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+            if (e != hipSuccess) return e;
+            raised = true;
+        }
+    }
     if (e0 || e1) {
         hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
                               P);
