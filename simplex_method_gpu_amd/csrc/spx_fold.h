@@ -34,6 +34,7 @@ typedef double fdbl2 __attribute__((ext_vector_type(2)));
 
 template <int KW>
 constexpr int FOLD_NP = KW + 2;  // LDS pitch of the staged coefficients
+constexpr int FOLD_THREADS_H = 512;  // = FOLD_THREADS (below): threads of a fold workgroup
 // LDS pitch of Rl: 72 doubles put the four k-rows of an MFMA operand read on
 // different banks (fold2_bench: -2 % against 64)
 constexpr int FOLD_RP = 72;
@@ -50,6 +51,47 @@ __device__ __forceinline__ void fold_stage_N(const double* Urows, int nf, double
     for (int k = threadIdx.x; k < KW * KW; k += blockDim.x) {
         const int t = k / KW, s = k % KW;
         NT[s][t] = (t < nf && s < t) ? Urows[k] : 0.0;
+    }
+}
+
+// The rebuild's operands, requested before the first tiles (vmcnt retires in
+// issue order, so loads issued behind the tile prefetch would wait for it):
+// the coefficients Urows (thread-strided) and, per lane of waves 0-3, the base
+// rows of R for its column (rows 4 u + g).  Unconditional loads with clamped
+// indices, so the compiler's waits count exactly; zeroed where unused when
+// consumed.
+template <int KW>
+struct FoldRPre {
+    static constexpr int NPT = (KW * KW + FOLD_THREADS_H - 1) / FOLD_THREADS_H;
+    double n[NPT];
+    double q[KW / 4];
+};
+template <int KW>
+__device__ __forceinline__ void fold_r_load(const double* Urows, const double* Qrows, int64_t L, int64_t c0,
+                                            FoldRPre<KW>& r) {
+    const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+    for (int j = 0; j < FoldRPre<KW>::NPT; ++j) {
+        const int k = tid + j * FOLD_THREADS_H;
+        r.n[j] = Urows[k < KW * KW ? k : KW * KW - 1];
+    }
+    const int g = lane & 3;
+    const int col = (16 * (tid >> 6) + (lane >> 2)) & 63;
+#pragma unroll
+    for (int u = 0; u < KW / 4; ++u) r.q[u] = Qrows[(int64_t)(4 * u + g) * L + c0 + col];
+}
+// fold_stage_N from the preloaded coefficients
+template <int KW>
+__device__ __forceinline__ void fold_stage_N_pre(const FoldRPre<KW>& r, int nf, double (&NT)[KW][FOLD_NP<KW>]) {
+#pragma unroll
+    for (int j = 0; j < FoldRPre<KW>::NPT; ++j) {
+        const int k = threadIdx.x + j * FOLD_THREADS_H;
+        // (no range test when the threads tile KW x KW exactly: a guarded
+        // store let the compiler sink the load into the guard and wait there)
+        if ((KW * KW) % FOLD_THREADS_H == 0 || k < KW * KW) {
+            const int t = k / KW, s = k % KW;
+            NT[s][t] = (t < nf && s < t) ? r.n[j] : 0.0;
+        }
     }
 }
 
@@ -73,7 +115,8 @@ __device__ __forceinline__ double quad_dpp(double v) {
 // operand latency: ~28 us of a C3 fold; this form 21-24 us with the loads.)
 template <int KW, int RP>
 __device__ __forceinline__ void fold_rebuild_R4(const double* Qrows, const double (&NT)[KW][FOLD_NP<KW>], int nf,
-                                                int64_t L, int64_t c0, double (&Rl)[KW][RP]) {
+                                                int64_t L, int64_t c0, double (&Rl)[KW][RP],
+                                                const FoldRPre<KW>* pre = nullptr) {
     constexpr int TG = KW / 4;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -84,7 +127,7 @@ __device__ __forceinline__ void fold_rebuild_R4(const double* Qrows, const doubl
 #pragma unroll
     for (int u = 0; u < TG; ++u) {
         const int t = 4 * u + g;
-        R[u] = (t < nf) ? Qrows[(int64_t)t * L + c0 + col] : 0.0;
+        R[u] = (t < nf) ? (pre ? pre->q[u] : Qrows[(int64_t)t * L + c0 + col]) : 0.0;
     }
 #pragma unroll
     for (int s = 0; s < KW; ++s) {
@@ -142,42 +185,70 @@ __device__ __forceinline__ void fold_tile_store(double* B, int64_t L, int64_t c0
     }
 }
 
-// U fragment (MFMA A operand) of the tile at rows r0..: lane holds
-// U[r0 + cl][4 s2 + kr] (0 past i1 or nf).
-template <int KW>
-__device__ __forceinline__ void fold_ufrag_load(const double* U, int nf, int64_t r0, int64_t i1,
-                                                double (&af)[KW / 4]) {
-    const int lane = threadIdx.x & 63;
-    const int kr = lane >> 4, cl = lane & 15;
-    const int64_t ia = r0 + cl;
-#pragma unroll
-    for (int s2 = 0; s2 < KW / 4; ++s2) {
-        const int t = 4 * s2 + kr;
-        af[s2] = (ia < i1 && t < nf) ? U[ia * KW + t] : 0.0;
-    }
-}
-
-// A wave's first tile (B rows and U fragment), loaded before the R rebuild.
+// A tile's operands as loaded: the B rows as the raw 16-byte loads and the
+// U fragment (MFMA A operand: lane holds U[r0 + cl][4 s2 + kr]).  Issued
+// unconditionally with rows clamped into the range, and only turned into the
+// accumulator layout (rows past i1 and pivots past nf zeroed) when the tile
+// is taken: moving a loaded value into another register waits for the load,
+// so unpacking at issue time made every load of the prefetch wait in turn.
 template <int KW>
 struct FoldTilePre {
-    dbl4 b[4];
+    fdbl2 b[4][2];
     double u[KW / 4];
 };
 template <int KW>
+__device__ __forceinline__ void fold_tile_issue(const double* B, const double* U, int64_t L, int64_t c0, int64_t r0,
+                                                int64_t i1, FoldTilePre<KW>& t) {
+    const int lane = threadIdx.x & 63;
+    const int kr = lane >> 4, cl = lane & 15;
+    const int64_t ilast = i1 > 0 ? i1 - 1 : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i0r = r0 + kr + 4 * r;
+        const int64_t i = i0r < ilast ? i0r : ilast;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) t.b[r][h] = *reinterpret_cast<const fdbl2*>(&B[i * L + c0 + 32 * h + 2 * cl]);
+    }
+    const int64_t ia0 = r0 + cl;
+    const int64_t ia = ia0 < ilast ? ia0 : ilast;
+#pragma unroll
+    for (int s2 = 0; s2 < KW / 4; ++s2) t.u[s2] = U[ia * KW + 4 * s2 + kr];
+}
+template <int KW>
+__device__ __forceinline__ void fold_tile_take(const FoldTilePre<KW>& t, int64_t r0, int64_t i1, int nf, dbl4 (&acc)[4],
+                                               double (&af)[KW / 4]) {
+    const int lane = threadIdx.x & 63;
+    const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool ok = r0 + kr + 4 * r < i1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            acc[2 * h][r] = ok ? t.b[r][h].x : 0.0;
+            acc[2 * h + 1][r] = ok ? t.b[r][h].y : 0.0;
+        }
+    }
+    const bool oka = r0 + cl < i1;
+#pragma unroll
+    for (int s2 = 0; s2 < KW / 4; ++s2) af[s2] = (oka && 4 * s2 + kr < nf) ? t.u[s2] : 0.0;
+}
+
+// A wave's first tile, requested before the R rebuild.
+template <int KW>
 __device__ __forceinline__ void fold_tile_first(const double* B, const double* U, int nf, int64_t L, int64_t c0,
                                                 int64_t i0, int64_t i1, FoldTilePre<KW>& pre) {
+    (void)nf;
     const int64_t r0 = i0 + 16 * (int64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (r0 >= i1) return;
-    fold_ufrag_load<KW>(U, nf, r0, i1, pre.u);
-    fold_tile_load(B, L, c0, r0, i1, pre.b);
+    fold_tile_issue<KW>(B, U, L, c0, r0, i1, pre);
 }
 
 // B[i0:i1, stripe c0] += U[i0:i1, 0:nf] R[0:nf, stripe] with 16x16 fp64 MFMA
 // tiles (the B tile is the accumulator); U is m x KW row-major.  Wave w takes
-// tiles i0 + 16 w, i0 + 16 (w + nwaves), ..  The next tile's U fragment and B
-// rows are issued after this tile's operands were taken: vmcnt retires in
-// issue order, and U fragments loaded per tile after the next tile's B loads
-// (the previous form) made every tile's MFMAs wait for that whole prefetch.
+// tiles i0 + 16 w, i0 + 16 (w + nwaves), ..  The next tile's operands are
+// issued once this tile's are taken, before its MFMAs; every tile but the
+// wave's last is whole (ranges are whole tiles up to m), so in the loop the
+// loads and stores are unconditional and the compiler's waits exact (the next
+// tile's loads wait for this tile's loads, not for its stores).
 // first: the wave's first tile (fold_tile_first) when have_first.  Call
 // after a barrier that published Rl.
 template <int KW, int RP>
@@ -191,35 +262,18 @@ __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, i
     const int kr = lane >> 4, cl = lane & 15;
     int64_t r0 = i0 + 16 * wave;
     if (r0 >= i1) return;
-    dbl4 nb[4];
-    double nu[KS];
-    if (have_first) {
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) nb[jb] = first.b[jb];
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) nu[s2] = first.u[s2];
-    } else {
-        fold_ufrag_load<KW>(U, nf, r0, i1, nu);
-        fold_tile_load(B, L, c0, r0, i1, nb);
-    }
-    for (; r0 < i1; r0 += 16 * nwaves) {
-        dbl4 acc[4];
-        double af[KS];
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) acc[jb] = nb[jb];
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) af[s2] = nu[s2];
-        const int64_t rn = r0 + 16 * nwaves;
-        if (rn < i1) {
-            fold_ufrag_load<KW>(U, nf, rn, i1, nu);
-            fold_tile_load(B, L, c0, rn, i1, nb);
-        }
-        // R fragment (B operand) from LDS: R[4 s2 + kr][slot 16 jb + cl].  All
-        // KS k-steps run (rows t >= nf of R and U's columns past nf are exact
-        // zeros; a per-step nf branch kept the next step's LDS reads behind
-        // this step's MFMAs), one step's fragments read ahead: the schedule
-        // barrier keeps the compiler from hoisting every step's reads (256
-        // VGPRs, one workgroup per CU) or exposing each read's latency.
+    const int64_t step = 16 * (int64_t)nwaves;
+    const int nt = (int)((i1 - r0 + step - 1) / step);  // this wave's tiles
+    FoldTilePre<KW> cur;
+    if (have_first) cur = first;
+    else fold_tile_issue<KW>(B, U, L, c0, r0, i1, cur);
+    // R fragment (B operand) from LDS: R[4 s2 + kr][slot 16 jb + cl].  All KS
+    // k-steps run (rows t >= nf of R and U's columns past nf are exact zeros;
+    // a per-step nf branch kept the next step's LDS reads behind this step's
+    // MFMAs), one step's fragments read ahead: the schedule barrier keeps the
+    // compiler from hoisting every step's reads (256 VGPRs, one workgroup per
+    // CU) or exposing each read's latency.
+    auto mfmas = [&](dbl4 (&acc)[4], const double (&af)[KS]) {
         double rf[2][4];
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) rf[0][jb] = Rl[kr][16 * jb + cl];
@@ -234,8 +288,30 @@ __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, i
                 acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], rf[s2 & 1][jb], acc[jb], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        fold_tile_store(B, L, c0, r0, i1, acc);
+    };
+    for (int k = 0; k + 1 < nt; ++k, r0 += step) {  // whole tiles, next one in flight
+        dbl4 acc[4];
+        double af[KS];
+        fold_tile_take<KW>(cur, r0, i1, nf, acc, af);
+        fold_tile_issue<KW>(B, U, L, c0, r0 + step, i1, cur);
+        mfmas(acc, af);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = r0 + kr + 4 * r;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                fdbl2 v;
+                v.x = acc[2 * h][r];
+                v.y = acc[2 * h + 1][r];
+                *reinterpret_cast<fdbl2*>(&B[i * L + c0 + 32 * h + 2 * cl]) = v;
+            }
+        }
     }
+    dbl4 acc[4];  // the wave's last tile (rows past i1 neither read nor written)
+    double af[KS];
+    fold_tile_take<KW>(cur, r0, i1, nf, acc, af);
+    mfmas(acc, af);
+    fold_tile_store(B, L, c0, r0, i1, acc);
 }
 
 // Row ranges of a fold grid: gridDim.y ranges of whole 16-row tiles.
@@ -249,7 +325,7 @@ __device__ __forceinline__ void fold_rows(int64_t m, int64_t& i0, int64_t& i1) {
 // 0-3 rebuild R (fold_rebuild_R4) while 4-7 hold their first tiles, then all
 // eight walk tiles (fold2_bench, C3: 75.8 us against 81-84 us for 4-wave
 // workgroups at 1 or 2 per CU).
-constexpr int FOLD_THREADS = 512;
+constexpr int FOLD_THREADS = FOLD_THREADS_H;
 // Host: the row split of a fold grid over nx stripes — about one workgroup
 // per CU, at least one 16-row tile per wave.
 inline int64_t fold_grid_y(int64_t m, int nx, int cus) {

@@ -1619,12 +1619,16 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_fold(Params P, int min_nw) {
     int64_t i0, i1;
     fold_rows(P.m, i0, i1);
     // spx_fold.h: first tiles in flight, R rebuilt by all four waves, tiles
+    // (the rebuild's operands are requested ahead of the first tiles and the
+    // barriers wait for LDS only: the rebuild does not wait for the tiles)
+    FoldRPre<KW> rpre;
+    fold_r_load<KW>(P.Urows, P.Qrows, L, c0, rpre);
     FoldTilePre<KW> pre;
     fold_tile_first<KW>(P.B0, P.U, nf, L, c0, i0, i1, pre);
-    fold_stage_N<KW>(P.Urows, nf, NT);
-    __syncthreads();
-    if (tid < 256) fold_rebuild_R4<KW, FOLD_RP>(P.Qrows, NT, nf, L, c0, Rl);
-    __syncthreads();
+    fold_stage_N_pre<KW>(rpre, nf, NT);
+    lds_barrier();
+    if (tid < 256) fold_rebuild_R4<KW, FOLD_RP>(P.Qrows, NT, nf, L, c0, Rl, &rpre);
+    lds_barrier();
     fold_tiles<KW, FOLD_RP>(P.B0, P.U, nf, L, c0, i0, i1, Rl, pre, true);
     if (wave == 0 && blockIdx.y == 0) {
         // y_w += SY R for this stripe (t ascending, the rebuild's R)
