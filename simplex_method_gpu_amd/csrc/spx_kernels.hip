@@ -45,6 +45,9 @@ namespace spx {
 #ifndef SPX_LDS_BATCH
 #define SPX_LDS_BATCH 4  // eta-window pricing: y / base-row LDS reads issued together
 #endif
+#ifndef SPX_PRICE_PIPE
+#define SPX_PRICE_PIPE 1  // eta-window pricing: two 8-chunk batches of a column in flight
+#endif
 #ifndef SPX_WIN_APLDS
 #define SPX_WIN_APLDS 0  // eta-window FTRAN: A_p from LDS (1) or through L1/L2 (0)
 #endif
@@ -371,6 +374,45 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 a0 = fma(v.x, w.x, a0);
                 a1 = fma(v.y, w.y, a1);
             }
+        } else if (SPX_PRICE_PIPE && have && (L2 & 511) == 0) {
+            // two 8-chunk batches in flight inside a column: the next batch is
+            // requested before the current one is consumed (the prefetched
+            // first batch is consumed above; kb: the batch base, uniform).  The
+            // fma order is the loop's below (the same bits).
+            auto consume = [&](const dbl2 (&vc)[8], int64_t kb) {
+#pragma unroll
+                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
+                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH];
+#pragma unroll
+                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                        w[u] = Y(kb + lane + (h + u) * 64);
+                        r[u] = Rw(kb + lane + (h + u) * 64);
+                    }
+#pragma unroll
+                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                        a0 = fma(vc[h + u].x, w[u].x, a0);
+                        a1 = fma(vc[h + u].y, w[u].y, a1);
+                        b0 = fma(vc[h + u].x, r[u].x, b0);
+                        b1 = fma(vc[h + u].y, r[u].y, b1);
+                    }
+                }
+            };
+            if (L2 > 8 * 64) {
+                int64_t kb = 8 * 64;
+                dbl2 vc[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+                for (; kb + 8 * 64 < L2; kb += 8 * 64) {
+                    dbl2 vn[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
+                    consume(vc, kb);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) vc[u] = vn[u];
+                }
+                consume(vc, kb);
+            }
+            k = L2;
         } else {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
                 dbl2 v[8], w[8], r[8];
