@@ -356,7 +356,34 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
             k += CH * 64;
         }
-        if (!WIN || !pend) {
+        if ((!WIN || !pend) && SPX_PRICE_PIPE && have && (L2 & 511) == 0) {
+            // as the window branch below: the next 8-chunk batch requested
+            // before the current one is consumed (the same fma order)
+            if (L2 > 8 * 64) {
+                int64_t kb = 8 * 64;
+                dbl2 vc[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+                auto consume = [&](int64_t kq) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const dbl2 w = Y(kq + lane + u * 64);
+                        a0 = fma(vc[u].x, w.x, a0);
+                        a1 = fma(vc[u].y, w.y, a1);
+                    }
+                };
+                for (; kb + 8 * 64 < L2; kb += 8 * 64) {
+                    dbl2 vn[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
+                    consume(kb);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) vc[u] = vn[u];
+                }
+                consume(kb);
+            }
+            k = L2;
+        } else if (!WIN || !pend) {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
                 dbl2 v[8];
 #pragma unroll
