@@ -59,6 +59,47 @@ __device__ __forceinline__ void price_column(const dbl2* __restrict__ col, const
         }
         k += CH * 64;
     }
+#ifndef SPX_LOOP_PIPE
+#define SPX_LOOP_PIPE 1  // two 8-chunk batches of a column in flight (as k_price)
+#endif
+    if (SPX_LOOP_PIPE && (L2 & 511) == 0 && L2 > 8 * 64) {
+        // the next batch requested before the current one is consumed; the
+        // same fma order as the loop below
+        int64_t kb = have ? 8 * 64 : 0;
+        dbl2 vc[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+        auto consume = [&](int64_t kq) {
+#pragma unroll
+            for (int h = 0; h < 8; h += 4) {
+                dbl2 w[4], r[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    w[u] = Y[kq + lane + (h + u) * 64];
+                    if constexpr (PEND) r[u] = Rw[kq + lane + (h + u) * 64];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a0 = fma(vc[h + u].x, w[u].x, a0);
+                    a1 = fma(vc[h + u].y, w[u].y, a1);
+                    if constexpr (PEND) {
+                        b0 = fma(vc[h + u].x, r[u].x, b0);
+                        b1 = fma(vc[h + u].y, r[u].y, b1);
+                    }
+                }
+            }
+        };
+        for (; kb + 8 * 64 < L2; kb += 8 * 64) {
+            dbl2 vn[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
+            consume(kb);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vc[u] = vn[u];
+        }
+        consume(kb);
+        return;
+    }
     for (; k + 7 * 64 < L2; k += 8 * 64) {
         dbl2 v[8];
 #pragma unroll
