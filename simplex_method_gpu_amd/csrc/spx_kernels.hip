@@ -356,7 +356,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
             k += CH * 64;
         }
-        if ((!WIN || !pend) && SPX_PRICE_PIPE && have && (L2 & 511) == 0) {
+        if ((!WIN || !pend) && SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0) {
             // as the window branch below: the next 8-chunk batch requested
             // before the current one is consumed (the same fma order)
             if (L2 > 8 * 64) {
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 a0 = fma(v.x, w.x, a0);
                 a1 = fma(v.y, w.y, a1);
             }
-        } else if (SPX_PRICE_PIPE && have && (L2 & 511) == 0) {
+        } else if (SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0) {
             // two 8-chunk batches in flight inside a column: the next batch is
             // requested before the current one is consumed (the prefetched
             // first batch is consumed above; kb: the batch base, uniform).  The
