@@ -45,6 +45,9 @@ namespace spx {
 #ifndef SPX_LDS_BATCH
 #define SPX_LDS_BATCH 4  // eta-window pricing: y / base-row LDS reads issued together
 #endif
+#ifndef SPX_PRICE_CH
+#define SPX_PRICE_CH 8  // chunks of a column's start prefetched (8-wave workgroups)
+#endif
 #ifndef SPX_PRICE_PIPE
 #define SPX_PRICE_PIPE 1  // eta-window pricing: two 8-chunk batches of a column in flight
 #endif
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // which stay in flight across the LDS fill and the barrier.  Every load
     // here is unconditional with a clamped index (rr is always a valid row),
     // so the fill waits for its own loads only, not for the A prefetch.
-    constexpr int CH = 8;
+    constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
     const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
     dbl2 yv[YB], rv[YB];
     double uqrow = 0.0;  // U[q][tid] for Urows (window, workgroup 0)
@@ -359,8 +362,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if ((!WIN || !pend) && SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0) {
             // as the window branch below: the next 8-chunk batch requested
             // before the current one is consumed (the same fma order)
-            if (L2 > 8 * 64) {
-                int64_t kb = 8 * 64;
+            if (L2 > CH * 64) {
+                int64_t kb = CH * 64;
                 dbl2 vc[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
@@ -424,8 +427,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     }
                 }
             };
-            if (L2 > 8 * 64) {
-                int64_t kb = 8 * 64;
+            if (L2 > CH * 64) {
+                int64_t kb = CH * 64;
                 dbl2 vc[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);

@@ -6,7 +6,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"; mkdir -p gpurun_out/shardab
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/shardab/pytest.log 2>&1 || { tail -30 gpurun_out/shardab/pytest.log; exit 1; }
 tail -1 gpurun_out/shardab/pytest.log
-for v in default $1; do
+for v in default $1 $2; do
   if [ $v = default ]; then L=$ROOT/simplex_method_gpu_amd/libsimplex.so; else L=$ROOT/simplex_method_gpu_amd/_build/$v/libsimplex.so; fi
   SPX_LIB=$L timeout -k 10 300 python3 -u tools/shard_rehearsal.py --n 16384 > gpurun_out/shardab/$v.json || exit 1
   python3 -c "
