@@ -345,6 +345,55 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
         double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
         int64_t k = lane;
+        // Two 8-chunk batches in flight through the column: the batch after
+        // the prefetched first one is requested before that one is consumed,
+        // and every later batch before its predecessor is (kb: the batch
+        // base, uniform).  The fma order is the loop's below (the same bits).
+        const bool pipe = SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0 && L2 > CH * 64;
+        auto run_pipe = [&](auto pend_t) {
+            constexpr bool PD = decltype(pend_t)::value;
+            auto consume = [&](const dbl2* vv, int nb8, int64_t kb) {
+#pragma unroll
+                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
+                    if (h >= nb8) break;
+                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH];
+#pragma unroll
+                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                        w[u] = Y(kb + lane + (h + u) * 64);
+                        if constexpr (PD) r[u] = Rw(kb + lane + (h + u) * 64);
+                    }
+#pragma unroll
+                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                        a0 = fma(vv[h + u].x, w[u].x, a0);
+                        a1 = fma(vv[h + u].y, w[u].y, a1);
+                        if constexpr (PD) {
+                            b0 = fma(vv[h + u].x, r[u].x, b0);
+                            b1 = fma(vv[h + u].y, r[u].y, b1);
+                        }
+                    }
+                }
+            };
+            int64_t kb = CH * 64;
+            dbl2 vc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+            consume(v0, CH, 0);
+            for (; kb + 8 * 64 < L2; kb += 8 * 64) {
+                dbl2 vn[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
+                consume(vc, 8, kb);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vc[u] = vn[u];
+            }
+            consume(vc, 8, kb);
+            k = L2;
+        };
+        if (pipe && WIN && pend) {
+            run_pipe(std::true_type());
+        } else if (pipe) {
+            run_pipe(std::false_type());
+        } else {
         if (have) {  // consume the prefetched chunks (same k order as the loop)
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
@@ -359,34 +408,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
             k += CH * 64;
         }
-        if ((!WIN || !pend) && SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0) {
-            // as the window branch below: the next 8-chunk batch requested
-            // before the current one is consumed (the same fma order)
-            if (L2 > CH * 64) {
-                int64_t kb = CH * 64;
-                dbl2 vc[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
-                auto consume = [&](int64_t kq) {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const dbl2 w = Y(kq + lane + u * 64);
-                        a0 = fma(vc[u].x, w.x, a0);
-                        a1 = fma(vc[u].y, w.y, a1);
-                    }
-                };
-                for (; kb + 8 * 64 < L2; kb += 8 * 64) {
-                    dbl2 vn[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
-                    consume(kb);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) vc[u] = vn[u];
-                }
-                consume(kb);
-            }
-            k = L2;
-        } else if (!WIN || !pend) {
+        if (!WIN || !pend) {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
                 dbl2 v[8];
 #pragma unroll
@@ -404,45 +426,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 a0 = fma(v.x, w.x, a0);
                 a1 = fma(v.y, w.y, a1);
             }
-        } else if (SPX_PRICE_PIPE && BLOCK <= 512 && have && (L2 & 511) == 0) {
-            // two 8-chunk batches in flight inside a column: the next batch is
-            // requested before the current one is consumed (the prefetched
-            // first batch is consumed above; kb: the batch base, uniform).  The
-            // fma order is the loop's below (the same bits).
-            auto consume = [&](const dbl2 (&vc)[8], int64_t kb) {
-#pragma unroll
-                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
-                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH];
-#pragma unroll
-                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
-                        w[u] = Y(kb + lane + (h + u) * 64);
-                        r[u] = Rw(kb + lane + (h + u) * 64);
-                    }
-#pragma unroll
-                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
-                        a0 = fma(vc[h + u].x, w[u].x, a0);
-                        a1 = fma(vc[h + u].y, w[u].y, a1);
-                        b0 = fma(vc[h + u].x, r[u].x, b0);
-                        b1 = fma(vc[h + u].y, r[u].y, b1);
-                    }
-                }
-            };
-            if (L2 > CH * 64) {
-                int64_t kb = CH * 64;
-                dbl2 vc[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
-                for (; kb + 8 * 64 < L2; kb += 8 * 64) {
-                    dbl2 vn[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) vn[u] = ld2<SPX_NT_A>(&col[kb + 8 * 64 + lane + u * 64]);
-                    consume(vc, kb);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) vc[u] = vn[u];
-                }
-                consume(vc, kb);
-            }
-            k = L2;
         } else {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
                 dbl2 v[8], w[8], r[8];
@@ -475,6 +458,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 b0 = fma(v.x, r.x, b0);
                 b1 = fma(v.y, r.y, b1);
             }
+        }
         }
         // next column's first chunks in flight during this column's reduction
         const int nidx = idx + stride;
