@@ -25,7 +25,8 @@ N>1.  `--row-shard` instead row-shards an explicit B^-1
 (SURVEY.md §8f row 1).  The job does one iteration per step on a fixed LP
 ("strong" scaling); `pricing` reports the aggregate pricing throughput (all
 ranks' algorithmic pricing bytes / max-over-ranks of pricing kernel + MINLOC
-time).
+time); `pricing_c4` measures the same on the north-star pricing-scaling config
+(C4, m=4096 n=131072) at every N, so the SCALE lines give its 1 -> N speedup.
 
 roofline: the pricing kernel (dominant: 60 % of the algorithmic bytes at C3),
 algorithmic bytes = 8*(m+1)*(non-basic columns priced on this rank) per launch,
@@ -76,6 +77,8 @@ def parse():
                     help="N > 1: row-shard an explicit B^-1 over the ranks (SURVEY.md §8f row 1) "
                          "instead of replicating the eta window")
     ap.add_argument("--no-explicit", action="store_true", help="skip the explicit-B^-1 block")
+    ap.add_argument("--no-sharded-pricing", action="store_true",
+                    help="skip the C4 column-sharded pricing block (pricing_c4)")
     ap.add_argument("--no-tableau", action="store_true",
                     help="skip the window-tableau measurement (the `tableau` block, one GPU only)")
     ap.add_argument("--comm1", action="store_true",
@@ -121,8 +124,8 @@ def main():
     m, n = args.m, args.n
     row_shard = multi and args.row_shard
 
-    def make(timing, window):
-        ctx = spx.Context(m=m, n=n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
+    def make(timing, window, mm=None, nn=None):
+        ctx = spx.Context(m=mm or m, n=nn or n, seed=args.seed, device=local, rank=rank, nranks=world, timing=timing,
                           update_rows=args.update_rows, update_block=args.update_block,
                           price_block=args.price_block, graph_batch=args.graph_batch,
                           row_shard=row_shard and window < 0, window=window,
@@ -249,6 +252,10 @@ def main():
     if not args.no_explicit and win > 0 and not row_shard:
         explicit = explicit_block(timed_window, kernel_split, reduce_max, m, n)
 
+    sharded = None
+    if not args.no_sharded_pricing and (m, n) != CONFIGS["C4"]:
+        sharded = sharded_pricing_block(make, reduce_max, reduce_sum, world, args)
+
     tab = None
     if world == 1 and not multi and not args.no_tableau:
         tab = tableau_block(spx, torch, m, n, args, local)
@@ -335,12 +342,50 @@ def main():
                 "max_rank_update_ms": update_ms_max,
             },
             "explicit": explicit,
+            "pricing_c4": sharded,
             "tableau": tab,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if multi:
         dist.destroy_process_group()
+
+
+def sharded_pricing_block(make, reduce_max, reduce_sum, world, args):
+    """The north-star pricing-scaling config (BASELINE.json configs[3], C4:
+    m=4096, n=131072, columns sharded over the ranks, RCCL all-gather MINLOC):
+    each rank's pricing kernel and pricing + MINLOC exchange event-timed over
+    one whole window of pivots; aggregate pricing throughput = all ranks'
+    algorithmic pricing bytes / the max over ranks of pricing + MINLOC.  Run
+    at every N, so SCALE's lines give the 1 -> N pricing speedup directly."""
+    m4, n4 = CONFIGS["C4"]
+    ctx = make(True, 0, m4, n4)
+    try:
+        cfg = ctx.config()
+        per = max(cfg["window"] - 1, 1)
+        ctx.iterate(args.warmup)
+        ds = ctx.dispatch_stats()
+        if cfg["window"] and ds["window_pos"] < cfg["window"]:
+            ctx.iterate(cfg["window"] - ds["window_pos"])
+        ctx.pass_times()
+        info0 = ctx.info()
+        ctx.iterate(per)
+        pt = ctx.pass_times()
+        info1 = ctx.info()
+    finally:
+        ctx.close()
+    passes = max(pt["passes"], 1)
+    price_ms = pt["price_ms"] / passes
+    pm_ms = pt["price_minloc_ms"] / passes
+    nb = 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"])
+    bytes_rank = 8.0 * (m4 + 1) * nb
+    price_max, pm_max = reduce_max([price_ms, pm_ms])
+    bytes_all = reduce_sum([bytes_rank])[0]
+    return {"config": f"C4 m={m4} n={n4}, pricing columns sharded over {world} rank(s)",
+            "passes_timed": int(pt["passes"]), "bytes_all_ranks": bytes_all,
+            "max_rank_price_ms": price_max, "max_rank_price_plus_minloc_ms": pm_max,
+            "throughput_GBps": bytes_all / (pm_max * 1e-3) / 1e9 if pm_max > 0 else 0.0,
+            "price_kernel_GBps_per_rank": bytes_rank / (price_ms * 1e-3) / 1e9 if price_ms > 0 else 0.0}
 
 
 def explicit_block(timed_window, kernel_split, reduce_max, m, n):
