@@ -159,10 +159,12 @@ typedef struct spx_opts {
                                 FTRAN the column T_w[:, p].  Needs the window (0 =
                                 auto selects 64) and one rank; twice A's memory. */
 #define SPX_FLAG_COUNTED_TAIL 512 /* tuning: the update kernel's workgroups hand
-                                     their ratio-test partials to the tail by
-                                     drained stores + a last-arrival count
-                                     instead of tagged words polled by the
-                                     last workgroup (the default)             */
+                                     their ratio-test partials (and the pricing
+                                     kernel's, where it reduces them itself)
+                                     to the tail by drained stores + a
+                                     last-arrival count instead of tagged
+                                     words polled by the last workgroup (the
+                                     default)                                 */
 #define SPX_FLAG_PRICE_TAIL 1024 /* tuning: the pricing kernel's last workgroup
                                     merges the entering candidates (default on
                                     one rank with the window: every update

@@ -424,6 +424,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.upd_soa, (size_t)(7 * uc.grid)));
     if (!P.row_shard && !P.tab && !(x->opts.flags & SPX_FLAG_COUNTED_TAIL))
         SPX_TRY(x->alloc(&P.upd_tag, (size_t)(UPD_WORDS * uc.grid)));
+    P.price_cap = pc.grid;
+    if (!P.tab && !(x->opts.flags & SPX_FLAG_COUNTED_TAIL))
+        SPX_TRY(x->alloc(&P.price_tag, (size_t)(PRICE_WORDS * pc.grid)));
     // the persistent loop kernel replaces the two-kernel pass where it applies
     if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {

@@ -115,6 +115,8 @@ constexpr int ARR_LINES = 1 + ARR_SHARDS;
 enum : int { ARR_PRICE = 0, ARR_UPDATE = 1, ARR_FOLD = 2, ARR_GROUPS = 3 };
 // tagged ratio-test partial: 7 eight-byte fields as 14 {32-bit half, tag} words
 constexpr int UPD_WORDS = 14;
+// tagged pricing partial (k_price's own tail): 4 eight-byte fields as 8 words
+constexpr int PRICE_WORDS = 8;
 
 struct alignas(16) DevState {
     int32_t status;      // ST_*
@@ -180,6 +182,11 @@ struct Params {
     // polled by the last workgroup instead of a drain + last-arrival count;
     // nullptr: the counted hand-off (upd_soa + arrive)
     uint64_t* upd_tag;
+    // k_price partials as tagged words (PRICE_WORDS per slot, field-major) for
+    // the pricing tail k_price itself runs (multi-rank, stepping API);
+    // nullptr: the counted hand-off (price_partials + arrive)
+    uint64_t* price_tag;
+    int64_t price_cap;
     DevState* st;
     // row-sharded B^-1 (nranks > 1 with SPX_FLAG_ROW_SHARD): this rank owns
     // global rows [r0, r0 + mloc) of B^-1, stored as B0/B1 (mloc x L ping-pong)

@@ -497,6 +497,89 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         return;
     }
+    if (P.price_tag) {
+        // Tagged hand-off (as k_update's, upd_publish_tagged): wave 0
+        // publishes the workgroup's partial as PRICE_WORDS {32-bit half, tag}
+        // words with one sc1 store instruction, and the last workgroup polls
+        // every slot until its words carry this pass's tag -- no drain and no
+        // last-arrival count.  The winner's new Wt entry travels in the
+        // partial; its earlier window entries were written by earlier kernels.
+        const uint32_t tag = (uint32_t)(it + 1);
+        if (wave == 0) {
+            PricePartial w = red[0];
+            for (int i = 1; i < WAVES; ++i)
+                if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
+            if (lane < PRICE_WORDS) {
+                const int f = lane >> 1;
+                const uint64_t u = f == 0 ? (uint64_t)__double_as_longlong(w.val)
+                                 : f == 1 ? (uint64_t)w.idx
+                                 : f == 2 ? (uint64_t)__double_as_longlong(w.w)
+                                          : (uint64_t)__double_as_longlong(w.pad);
+                const uint32_t half = (lane & 1) ? (uint32_t)(u >> 32) : (uint32_t)u;
+                st_agent(&P.price_tag[(int64_t)lane * P.price_cap + blockIdx.x], ((uint64_t)tag << 32) | half);
+            }
+        }
+        if (blockIdx.x != gridDim.x - 1) return;
+        const unsigned long long t_tail = slot ? rtime() : 0;
+        __shared__ bool s_to;
+        if (tid == 0) s_to = false;
+        lds_barrier();
+        PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
+        for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
+            uint64_t wd[PRICE_WORDS];
+            bool ok = false;
+            for (uint32_t spins = 0; spins <= (1u << 20); ++spins) {
+#pragma unroll
+                for (int k = 0; k < PRICE_WORDS; ++k) wd[k] = ld_agent(&P.price_tag[(int64_t)k * P.price_cap + g]);
+                ok = true;
+#pragma unroll
+                for (int k = 0; k < PRICE_WORDS; ++k) ok = ok && (uint32_t)(wd[k] >> 32) == tag;
+                if (ok) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) {
+                s_to = true;  // (a benign race: every writer stores true)
+                break;
+            }
+            uint64_t f[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) f[k] = (wd[2 * k] & 0xffffffffull) | (wd[2 * k + 1] << 32);
+            const PricePartial v{__longlong_as_double((long long)f[0]), (int64_t)f[1],
+                                 __longlong_as_double((long long)f[2]), __longlong_as_double((long long)f[3])};
+            if (argmin_better(v.val, v.idx, w.val, w.idx)) w = v;
+#pragma unroll
+            for (int k = 0; k < PRICE_WORDS; ++k) P.price_tag[(int64_t)k * P.price_cap + g] = 0ull;
+        }
+        // wave DPP argmin; the winner's payload from its lane
+        double bv = w.val;
+        int64_t bj = w.idx;
+        lane_argmin<64>(bv, bj);
+        bv = readlane_d(bv, 63);
+        bj = readlane_l(bj, 63);
+        const uint64_t hit = __ballot(w.val == bv && w.idx == bj);
+        const int wl = hit ? (int)__builtin_ctzll(hit) : 0;
+        const PricePartial o{bv, bj, readlane_d(w.w, wl), readlane_d(w.pad, wl)};
+        if (lane == 0) red[wave] = o;
+        lds_barrier();
+        PricePartial t = red[0];
+        for (int i = 1; i < WAVES; ++i)
+            if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
+        if (s_to) {  // a partial never arrived (a fault elsewhere): stop loudly
+            if (tid == 0) st->status = ST_HANDOFF_TIMEOUT;
+            return;
+        }
+        if (tid == 0) {
+            P.price_out[0] = ArgMinEntry{t.val, t.idx};
+            if (WIN && P.devex) *P.dvx_e = t.pad;
+        }
+        if (WIN && P.nin > 1) {
+            double* wo = reinterpret_cast<double*>(P.price_out + 1);
+            if (tid < KW)
+                wo[tid] = (t.idx == INT64_MAX || tid >= nw) ? 0.0 : (tid == tau ? t.w : P.Wt[t.idx * KW + tid]);
+        }
+        stamp_tail(slot, t_tail, win);
+        return;
+    }
     if (tid == 0) {
         PricePartial w = red[0];
         for (int i = 1; i < WAVES; ++i)
@@ -1870,6 +1953,8 @@ __global__ void k_reset(Params P) {
     for (int64_t k = t0; k < ARR_GROUPS * ARR_LINES * ARR_STRIDE; k += stride) P.arrive[k] = 0u;
     if (P.upd_tag)
         for (int64_t k = t0; k < UPD_WORDS * P.upd_cap; k += stride) P.upd_tag[k] = 0ull;
+    if (P.price_tag)
+        for (int64_t k = t0; k < PRICE_WORDS * P.price_cap; k += stride) P.price_tag[k] = 0ull;
     for (int64_t j = t0; j < n; j += stride) {
         if (P.W) P.W[j] = 1.0;  // Devex reference framework
         int32_t pos = -1;
