@@ -185,18 +185,34 @@ __device__ __forceinline__ void fold_tile_store(double* B, int64_t L, int64_t c0
     }
 }
 
-// A tile's operands as loaded: the B rows as the raw 16-byte loads and the
-// U fragment (MFMA A operand: lane holds U[r0 + cl][4 s2 + kr]).  Issued
-// unconditionally with rows clamped into the range, and only turned into the
-// accumulator layout (rows past i1 and pivots past nf zeroed) when the tile
-// is taken: moving a loaded value into another register waits for the load,
-// so unpacking at issue time made every load of the prefetch wait in turn.
+// U fragments through LDS (SPX_FOLD_ULDS = 1): a tile's 16 x KW block of U is
+// contiguous, so it is loaded as KW / 8 coalesced 16-byte loads per lane and
+// staged in the wave's LDS block, from which each k-step reads its A operand
+// (lane (kr, cl): U[r0 + cl][4 s2 + kr]).  Read directly, every operand load
+// touched 16 rows x 32 B (16 segments per instruction): fold2_bench, C3, tiles
+// 62.1 us, 47.9 us with no U loads at all.
+#ifndef SPX_FOLD_ULDS
+#define SPX_FOLD_ULDS 1
+#endif
+template <int KW>
+constexpr int FOLD_UP = KW + 2;  // LDS pitch of a staged U block (16-byte rows, 2-way reads)
+
+// A tile's operands as loaded: the B rows as the raw 16-byte loads and U (the
+// MFMA A operand) raw as well.  Issued unconditionally with rows clamped into
+// the range, and only turned into the accumulator layout (rows past i1 and
+// pivots past nf zeroed) when the tile is taken: moving a loaded value into
+// another register waits for the load, so unpacking at issue time made every
+// load of the prefetch wait in turn.
 template <int KW>
 struct FoldTilePre {
     fdbl2 b[4][2];
-    double u[KW / 4];
+#if SPX_FOLD_ULDS
+    fdbl2 u[KW / 8];  // lane l, load j: U row r0 + (128 j + 2 l) / KW, column (2 l) % KW
+#else
+    double u[KW / 4];  // lane (kr, cl): U[r0 + cl][4 s2 + kr]
+#endif
 };
-template <int KW>
+template <int KW, bool LOADU = true>
 __device__ __forceinline__ void fold_tile_issue(const double* B, const double* U, int64_t L, int64_t c0, int64_t r0,
                                                 int64_t i1, FoldTilePre<KW>& t) {
     const int lane = threadIdx.x & 63;
@@ -209,14 +225,25 @@ __device__ __forceinline__ void fold_tile_issue(const double* B, const double* U
 #pragma unroll
         for (int h = 0; h < 2; ++h) t.b[r][h] = *reinterpret_cast<const fdbl2*>(&B[i * L + c0 + 32 * h + 2 * cl]);
     }
+#if SPX_FOLD_ULDS
+#pragma unroll
+    for (int j = 0; j < KW / 8; ++j) {
+        const int e = 128 * j + 2 * lane;
+        const int64_t ia0 = r0 + e / KW;
+        const int64_t ia = ia0 < ilast ? ia0 : ilast;
+        t.u[j] = LOADU ? *reinterpret_cast<const fdbl2*>(&U[ia * KW + e % KW]) : fdbl2{1e-3 * (j + 1), 2e-3};
+    }
+#else
     const int64_t ia0 = r0 + cl;
     const int64_t ia = ia0 < ilast ? ia0 : ilast;
 #pragma unroll
-    for (int s2 = 0; s2 < KW / 4; ++s2) t.u[s2] = U[ia * KW + 4 * s2 + kr];
+    for (int s2 = 0; s2 < KW / 4; ++s2) t.u[s2] = LOADU ? U[ia * KW + 4 * s2 + kr] : 1e-3 * (s2 + 1);
+#endif
 }
+// Us: the wave's LDS block (SPX_FOLD_ULDS; af unused) or af the A operand
 template <int KW>
 __device__ __forceinline__ void fold_tile_take(const FoldTilePre<KW>& t, int64_t r0, int64_t i1, int nf, dbl4 (&acc)[4],
-                                               double (&af)[KW / 4]) {
+                                               double (&af)[KW / 4], double (*Us)[FOLD_UP<KW>]) {
     const int lane = threadIdx.x & 63;
     const int kr = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -228,9 +255,26 @@ __device__ __forceinline__ void fold_tile_take(const FoldTilePre<KW>& t, int64_t
             acc[2 * h + 1][r] = ok ? t.b[r][h].y : 0.0;
         }
     }
+#if SPX_FOLD_ULDS
+    (void)af;
+    (void)kr;
+    (void)cl;
+#pragma unroll
+    for (int j = 0; j < KW / 8; ++j) {
+        const int e = 128 * j + 2 * lane;
+        const int row = e / KW, col = e % KW;
+        const bool ok = r0 + row < i1;
+        fdbl2 v;
+        v.x = (ok && col < nf) ? t.u[j].x : 0.0;
+        v.y = (ok && col + 1 < nf) ? t.u[j].y : 0.0;
+        *reinterpret_cast<fdbl2*>(&Us[row][col]) = v;
+    }
+#else
+    (void)Us;
     const bool oka = r0 + cl < i1;
 #pragma unroll
     for (int s2 = 0; s2 < KW / 4; ++s2) af[s2] = (oka && 4 * s2 + kr < nf) ? t.u[s2] : 0.0;
+#endif
 }
 
 // A wave's first tile, requested before the R rebuild.
@@ -251,7 +295,7 @@ __device__ __forceinline__ void fold_tile_first(const double* B, const double* U
 // tile's loads wait for this tile's loads, not for its stores).
 // first: the wave's first tile (fold_tile_first) when have_first.  Call
 // after a barrier that published Rl.
-template <int KW, int RP>
+template <int KW, int RP, bool LOADU = true>
 __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, int64_t L, int64_t c0, int64_t i0,
                                            int64_t i1, const double (&Rl)[KW][RP], const FoldTilePre<KW>& first,
                                            bool have_first) {
@@ -260,13 +304,21 @@ __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, i
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwaves = blockDim.x >> 6;
     const int kr = lane >> 4, cl = lane & 15;
+#if SPX_FOLD_ULDS
+    // one 16-row block of U per wave; only that wave writes and reads it, and
+    // its LDS operations complete in order, so no barrier guards it
+    __shared__ double Ush[FOLD_THREADS_H / 64][16][FOLD_UP<KW>];
+    double (*Us)[FOLD_UP<KW>] = Ush[wave];
+#else
+    double (*Us)[FOLD_UP<KW>] = nullptr;
+#endif
     int64_t r0 = i0 + 16 * wave;
     if (r0 >= i1) return;
     const int64_t step = 16 * (int64_t)nwaves;
     const int nt = (int)((i1 - r0 + step - 1) / step);  // this wave's tiles
     FoldTilePre<KW> cur;
     if (have_first) cur = first;
-    else fold_tile_issue<KW>(B, U, L, c0, r0, i1, cur);
+    else fold_tile_issue<KW, LOADU>(B, U, L, c0, r0, i1, cur);
     // R fragment (B operand) from LDS: R[4 s2 + kr][slot 16 jb + cl].  All KS
     // k-steps run (rows t >= nf of R and U's columns past nf are exact zeros;
     // a per-step nf branch kept the next step's LDS reads behind this step's
@@ -275,25 +327,37 @@ __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, i
     // CU) or exposing each read's latency.
     auto mfmas = [&](dbl4 (&acc)[4], const double (&af)[KS]) {
         double rf[2][4];
+#if SPX_FOLD_ULDS
+        double uf[2];
+        uf[0] = Us[cl][kr];
+#endif
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) rf[0][jb] = Rl[kr][16 * jb + cl];
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
             if (s2 + 1 < KS) {
+#if SPX_FOLD_ULDS
+                uf[(s2 + 1) & 1] = Us[cl][4 * (s2 + 1) + kr];
+#endif
 #pragma unroll
                 for (int jb = 0; jb < 4; ++jb) rf[(s2 + 1) & 1][jb] = Rl[4 * (s2 + 1) + kr][16 * jb + cl];
             }
+#if SPX_FOLD_ULDS
+            const double a = uf[s2 & 1];
+#else
+            const double a = af[s2];
+#endif
 #pragma unroll
             for (int jb = 0; jb < 4; ++jb)
-                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[s2], rf[s2 & 1][jb], acc[jb], 0, 0, 0);
+                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, rf[s2 & 1][jb], acc[jb], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
     for (int k = 0; k + 1 < nt; ++k, r0 += step) {  // whole tiles, next one in flight
         dbl4 acc[4];
         double af[KS];
-        fold_tile_take<KW>(cur, r0, i1, nf, acc, af);
-        fold_tile_issue<KW>(B, U, L, c0, r0 + step, i1, cur);
+        fold_tile_take<KW>(cur, r0, i1, nf, acc, af, Us);
+        fold_tile_issue<KW, LOADU>(B, U, L, c0, r0 + step, i1, cur);
         mfmas(acc, af);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -309,7 +373,7 @@ __device__ __forceinline__ void fold_tiles(double* B, const double* U, int nf, i
     }
     dbl4 acc[4];  // the wave's last tile (rows past i1 neither read nor written)
     double af[KS];
-    fold_tile_take<KW>(cur, r0, i1, nf, acc, af);
+    fold_tile_take<KW>(cur, r0, i1, nf, acc, af, Us);
     mfmas(acc, af);
     fold_tile_store(B, L, c0, r0, i1, acc);
 }

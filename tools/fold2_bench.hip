@@ -116,16 +116,19 @@ __global__ __launch_bounds__(BLK, MINB) void k_fold_v(double* B, const double* U
     }
     FoldTilePre<KW> pre;
     if (MODE == 1) fold_tile_first<KW>(B, U, nf, L, c0, i0, i1, pre);
-    if (MODE != 3) {
+    if (MODE != 3 && MODE != 5) {
         fold_stage_N<KW>(N, nf, NT);
         __syncthreads();
+        const long long t0 = wall_clock64();
         if (tid < 256) fold_rebuild_R4<KW, FOLD_RP>(Q, NT, nf, L, c0, Rl);
+        if (MODE == 2 && tid == 0) sink[L + blockIdx.x + gridDim.x * blockIdx.y] = (double)(wall_clock64() - t0);
     } else {
         for (int k = tid; k < KW * FOLD_RP; k += BLK) (&Rl[0][0])[k] = 0.0;
     }
     __syncthreads();
     if (MODE == 1) fold_tiles<KW, FOLD_RP>(B, U, nf, L, c0, i0, i1, Rl, pre, true);
     if (MODE == 3) fold_tiles<KW, FOLD_RP>(B, U, nf, L, c0, i0, i1, Rl, pre, false);
+    if (MODE == 5) fold_tiles<KW, FOLD_RP, false>(B, U, nf, L, c0, i0, i1, Rl, pre, false);
     if (MODE == 2 && Rl[tid & 63][tid >> 6] == 12345.0) sink[0] = 1.0;
 }
 
@@ -226,7 +229,18 @@ int main(int argc, char** argv) {
         RUN(0, "round-1 fold");
         RUN(1, "shipped fold (spx_fold.h)");
         RUN(2, "shipped rebuild only");
+        {
+            std::vector<double> h(nx * ny);
+            CK(hipMemcpy(h.data(), sink + L, nx * ny * 8, hipMemcpyDeviceToHost));
+            double a = 0.0, mx = 0.0;
+            for (double v : h) a += v / (nx * ny), mx = v > mx ? v : mx;
+            int khz = 0;
+            CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+            std::printf("{\"kernel\": \"rebuild loop wave 0 (wall clock) ny=%d\", \"avg_us\": %.2f, \"max_us\": %.2f}\n", ny,
+                        a / khz * 1e3, mx / khz * 1e3);
+        }
         RUN(3, "shipped tiles only");
+        RUN(5, "tiles only, U fragments not loaded");
         std::snprintf(nm, sizeof nm, "shipped fold, 4-wave workgroups ny=%d", ny);
         timeit(nm, [&] { hipLaunchKernelGGL((k_fold_v<1, 256, 1>), dim3(nx, ny), dim3(256), 0, 0, B, U, Q, N, nf, m, L, sink); });
         std::snprintf(nm, sizeof nm, "memprobe round-1 tile pattern (8 B/lane) ny=%d", ny);
