@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--comm1", action="store_true",
                     help="rehearsal on one GPU: run the multi-rank path (torch.distributed + RCCL "
                          "MINLOC) with a one-rank communicator")
+    ap.add_argument("--minloc", choices=["rccl", "mbox"], default="rccl",
+                    help="N > 1: the pricing MINLOC exchange as an RCCL all-gather (default) or as direct "
+                         "stores into the peers' mailboxes (spx_mbox_attach, one small kernel per pass)")
     a = ap.parse_args()
     m, n = CONFIGS[a.config or "C3"]
     a.m = a.m or m
@@ -130,10 +133,14 @@ def main():
                           price_block=args.price_block, graph_batch=args.graph_batch,
                           row_shard=row_shard and window < 0, window=window,
                           comm1=(args.comm1 and world == 1))
-        if multi:
+        if multi and (args.minloc == "rccl" or (row_shard and window < 0)):
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             ctx.attach_comm(obj[0])
+        if multi and args.minloc == "mbox":  # MINLOC by k_exchange through the peer mailboxes
+            hs = [None] * world
+            dist.all_gather_object(hs, ctx.mbox_export())
+            ctx.mbox_attach(hs)
         return ctx
 
     def barrier():
@@ -288,7 +295,9 @@ def main():
                 "b_inverse": rep,
                 "geometry": cfg,
                 "m": m, "n": n, "seed": args.seed,
-                "parallelism": ((f"pricing column-sharded x{world} (RCCL all-gather MINLOC), " +
+                "parallelism": ((f"pricing column-sharded x{world} " +
+                                 ("(RCCL all-gather MINLOC), " if args.minloc == "rccl" else
+                                  "(MINLOC through peer mailboxes, k_exchange), ") +
                                  ("explicit B^-1 row-sharded (pivot row in a 2nd all-gather)" if row_shard else
                                   "B^-1 replicated"))
                                 if multi else "single GPU"),

@@ -195,6 +195,22 @@ void spx_destroy(spx_ctx* ctx);
 int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]);
 int spx_attach_comm(spx_ctx* ctx, const uint8_t id[SPX_COMM_ID_BYTES]);
 
+/* Peer mailboxes: the pricing MINLOC exchange (the RCCL all-gather of the
+ * candidate records after src/v4_cub_reduction.cu:294-302's argmin) as direct
+ * stores into every rank's device mailbox over xGMI, one small kernel per pass
+ * (k_exchange), instead of ncclAllGather.  Every rank calls spx_mbox_export,
+ * gathers all handles in rank order out of band (e.g. torch.distributed
+ * all_gather_object) and calls spx_mbox_attach with them; from then on the
+ * MINLOC exchange goes through the mailboxes.  The row-sharded B^-1 still
+ * needs spx_attach_comm (its ratio-test exchange is RCCL).  Collective in
+ * effect: all ranks must attach before any of them iterates.  Handles are
+ * hipIpcMemHandle_t bytes; a rank's own handle is not opened (its mailbox is
+ * used directly), so one rank (SPX_FLAG_COMM1) runs the same kernel alone.
+ * Ranks may share a device (several processes on one GPU). */
+#define SPX_MBOX_HANDLE_BYTES 64
+int spx_mbox_export(spx_ctx* ctx, uint8_t handle[SPX_MBOX_HANDLE_BYTES]);
+int spx_mbox_attach(spx_ctx* ctx, const uint8_t* handles /* nranks x SPX_MBOX_HANDLE_BYTES */);
+
 /* In-process shard group: G contexts created with nranks = G and ranks
  * 0..G-1 (any devices, no communicator) run k lockstep iterations with the
  * MINLOC candidates exchanged by device-to-device copies instead of RCCL

@@ -35,6 +35,7 @@ FLAG_SPLIT_TAIL = 16
 FLAG_NO_PERSIST = 32
 FLAG_PERSIST = 64  # force the persistent loop kernel where it applies (default: auto)
 FLAG_COMM1 = 128  # one rank through the RCCL path (tests)
+MBOX_HANDLE_BYTES = 64  # SPX_MBOX_HANDLE_BYTES
 FLAG_TABLEAU = 256  # window tableau: T_w = B_w A and dw kept beside the eta window
 FLAG_COUNTED_TAIL = 512  # ratio-test hand-off by drained stores + last-arrival count (default: tagged poll)
 FLAG_PRICE_TAIL = 1024  # k_price's last workgroup merges the entering candidates (default: deferred into k_update)
@@ -192,6 +193,21 @@ class Context:
     def attach_comm(self, uid: bytes):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self._L.spx_attach_comm(self._h, buf))
+
+    def mbox_export(self) -> bytes:
+        """This rank's mailbox handle (spx_mbox_export): gather every rank's
+        in rank order and pass the list to :meth:`mbox_attach`."""
+        buf = (ctypes.c_uint8 * MBOX_HANDLE_BYTES)()
+        check(self._L.spx_mbox_export(self._h, buf))
+        return bytes(buf)
+
+    def mbox_attach(self, handles):
+        """MINLOC through the peer mailboxes from now on (spx_mbox_attach)."""
+        blob = b"".join(handles)
+        if len(blob) != MBOX_HANDLE_BYTES * len(handles):
+            raise ValueError("mailbox handles are %d bytes each" % MBOX_HANDLE_BYTES)
+        buf = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(self._L.spx_mbox_attach(self._h, buf))
 
     def reset(self):
         check(self._L.spx_reset(self._h))

@@ -105,6 +105,12 @@ struct spx_ctx {
     bool comm_ready = false;
     bool use_comm = false;  // MINLOC through RCCL: nranks > 1, or SPX_FLAG_COMM1 (one-rank test of that path)
     bool graph_fallback = false;  // a capture with RCCL calls failed: eager passes
+    // peer mailboxes (spx_mbox_export / spx_mbox_attach): MINLOC by k_exchange
+    uint64_t* mbox = nullptr;
+    uint32_t* mbox_seq = nullptr;
+    uint64_t** mbox_peer = nullptr;  // device array of nranks mailbox pointers
+    std::vector<void*> mbox_opened;  // IPC mappings of the other ranks' mailboxes
+    bool mbox_ready = false;
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
 
     // graph replay of `batch` passes
@@ -605,14 +611,19 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     Pp.defer_price = x->defer_ok ? 1 : 0;
     HIP_TRY(launch_price(Pp, x->pcfg, x->stream, p0, p1));
     if (x->use_comm) {
-        if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
-        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
-                               x->stream));
+        if (x->mbox_ready) {
+            HIP_TRY(launch_exchange(x->P, x->stream));
+        } else {
+            if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but neither spx_attach_comm nor spx_mbox_attach was called");
+            NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
+                                   x->stream));
+        }
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(Pp, x->ucfg, x->stream, u0, u1));
     if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
     if (x->P.row_shard) {  // ratio-test all-gather (header + candidate row), then finalise
+        if (!x->comm_ready) return fail(SPX_ERR_STATE, "row-sharded B^-1 needs spx_attach_comm");
         NCCL_TRY(ncclAllGather(x->P.rs_send, x->rs_recv, (size_t)x->P.rs_stride, ncclUint8, x->comm, x->stream));
         HIP_TRY(launch_finalize_rs(x->P, x->stream));
     }
@@ -621,7 +632,8 @@ int enqueue_pass(spx_ctx* x, bool timed) {
 
 int build_graph(spx_ctx* x) {
     if (x->graph_exec || x->batch <= 0) return SPX_OK;
-    if (x->use_comm && !x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
+    if (x->use_comm && !x->comm_ready && !x->mbox_ready)
+        return fail(SPX_ERR_STATE, "nranks > 1 but neither spx_attach_comm nor spx_mbox_attach was called");
     HIP_TRY(hipStreamBeginCapture(x->stream, hipStreamCaptureModeThreadLocal));
     int rc = SPX_OK;
     const int nw_keep = x->nw;
@@ -1011,6 +1023,7 @@ void spx_destroy(spx_ctx* x) {
     for (hipEvent_t e : x->ev_loop) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->ev_fold) (void)hipEventDestroy(e);
     if (x->comm) (void)ncclCommDestroy(x->comm);
+    for (void* p : x->mbox_opened) (void)hipIpcCloseMemHandle(p);
     for (void* p : x->allocs) (void)hipFree(p);
     if (x->st_host) (void)hipHostFree(x->st_host);
     if (x->limit_host) (void)hipHostFree(x->limit_host);
@@ -1037,6 +1050,63 @@ int spx_attach_comm(spx_ctx* x, const uint8_t id[SPX_COMM_ID_BYTES]) {
     HIP_TRY(hipSetDevice(x->device));
     NCCL_TRY(ncclCommInitRank(&x->comm, x->opts.nranks, u, x->opts.rank));
     x->comm_ready = true;
+    return SPX_OK;
+}
+
+int spx_mbox_export(spx_ctx* x, uint8_t handle[SPX_MBOX_HANDLE_BYTES]) {
+    if (!x || !handle) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->use_comm) return fail(SPX_ERR_STATE, "mailboxes need opts.nranks > 1 (or SPX_FLAG_COMM1)");
+    static_assert(sizeof(hipIpcMemHandle_t) <= SPX_MBOX_HANDLE_BYTES, "hipIpcMemHandle_t too large");
+    HIP_TRY(hipSetDevice(x->device));
+    if (!x->mbox) {
+        // [2 parities][nranks][pr_stride * 4 halves] tagged words, zeroed (seq starts at 1);
+        // fine-grained and uncached: peers store into it over xGMI while k_exchange polls
+        const size_t words = (size_t)2 * x->opts.nranks * x->P.pr_stride * (sizeof(ArgMinEntry) / 4);
+        SPX_TRY(x->alloc(&x->mbox, words, hipDeviceMallocUncached));
+        SPX_TRY(x->alloc(&x->mbox_seq, 1));
+        HIP_TRY(hipStreamSynchronize(x->stream));
+    }
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, x->mbox));
+    std::memset(handle, 0, SPX_MBOX_HANDLE_BYTES);
+    std::memcpy(handle, &h, sizeof(h));
+    return SPX_OK;
+}
+
+int spx_mbox_attach(spx_ctx* x, const uint8_t* handles) {
+    if (!x || !handles) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->mbox) return fail(SPX_ERR_STATE, "spx_mbox_export first");
+    if (x->mbox_ready) return fail(SPX_ERR_STATE, "mailboxes already attached");
+    HIP_TRY(hipSetDevice(x->device));
+    const int G = x->opts.nranks;
+    std::vector<uint64_t*> peers((size_t)G);
+    for (int g = 0; g < G; ++g) {
+        if (g == x->opts.rank) {
+            peers[(size_t)g] = x->mbox;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)g * SPX_MBOX_HANDLE_BYTES, sizeof(h));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipIpcOpenMemHandle(rank %d): %s", g, hipGetErrorString(e));
+        x->mbox_opened.push_back(p);
+        peers[(size_t)g] = static_cast<uint64_t*>(p);
+    }
+    SPX_TRY(x->alloc(&x->mbox_peer, (size_t)G));
+    HIP_TRY(hipMemcpyAsync(x->mbox_peer, peers.data(), sizeof(uint64_t*) * (size_t)G, hipMemcpyHostToDevice,
+                           x->stream));
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    x->P.mbox_peer = x->mbox_peer;
+    x->P.mbox = x->mbox;
+    x->P.mbox_seq = x->mbox_seq;
+    x->P.mbox_rank = x->opts.rank;
+    // a graph captured before (with the RCCL exchange, or none) is rebuilt
+    if (x->graph_exec) (void)hipGraphExecDestroy(x->graph_exec);
+    if (x->graph) (void)hipGraphDestroy(x->graph);
+    x->graph_exec = nullptr;
+    x->graph = nullptr;
+    x->mbox_ready = true;
     return SPX_OK;
 }
 
@@ -1315,8 +1385,12 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
     const int ps = x->P.pr_stride;
     if (x->use_comm) {
-        if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but spx_attach_comm was not called");
-        NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * ps, ncclUint8, x->comm, x->stream));
+        if (x->mbox_ready) {
+            HIP_TRY(launch_exchange(x->P, x->stream));
+        } else {
+            if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but neither spx_attach_comm nor spx_mbox_attach was called");
+            NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * ps, ncclUint8, x->comm, x->stream));
+        }
     }
     std::vector<ArgMinEntry> cand((size_t)x->opts.nranks * ps);
     HIP_TRY(hipStreamSynchronize(x->stream));

@@ -244,6 +244,17 @@ struct Params {
     // sharded last-arrival counters (spx_common.h arrive_last), ARR_GROUPS
     // groups of ARR_LINES 128-byte lines
     uint32_t* arrive;
+    // peer mailboxes (spx_mbox_attach): the MINLOC exchange as direct stores
+    // into every rank's mailbox (k_exchange) instead of an RCCL all-gather.
+    // Mailbox words: [2 parities][nin ranks][pr_stride * 4 halves], each
+    // (seq << 32) | 32-bit half of the record; mbox_peer[g] is rank g's
+    // mailbox as mapped here (IPC), mbox this rank's own, mbox_seq the
+    // exchange counter (every rank runs the same exchanges)
+    uint64_t* const* mbox_peer;
+    uint64_t* mbox;
+    uint32_t* mbox_seq;
+    int32_t mbox_rank;
+    int32_t pad_mb;
 };
 
 __device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {

@@ -29,6 +29,7 @@ hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n
 hipError_t launch_reset(const Params& P, hipStream_t s);
 hipError_t launch_flush(const Params& P, hipStream_t s);
 hipError_t launch_finalize_rs(const Params& P, hipStream_t s);
+hipError_t launch_exchange(const Params& P, hipStream_t s);
 hipError_t launch_tail(const Params& P, int nparts, hipStream_t s);
 hipError_t launch_materialize(const Params& P, double* out, hipStream_t s);
 hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s);

@@ -2107,6 +2107,70 @@ hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// MINLOC exchange through peer mailboxes (spx_mbox_attach): the replacement
+// for the all-gather of the candidate records (v4:294-302 runs the argmin on
+// one device; across ranks every rank needs every record).  One workgroup:
+// this rank's record (price_out, written by k_price) is stored as tagged
+// words into slot [seq & 1][rank] of every rank's mailbox, then the nin
+// slots of this rank's own mailbox are polled until every word carries seq
+// and unpacked into price_in, which k_update reads as it reads the RCCL
+// all-gather's output.  Each 8-byte word is stored and loaded whole, so a
+// record is complete when all its tags match, with no fence or flag.  Two
+// parities suffice: a rank reaches exchange seq + 2 only after every rank's
+// record of seq + 1, which each stored after consuming seq.  System-scope
+// stores and loads (the mailboxes are fine-grained, mapped over xGMI on other
+// devices).  A rank that polls for MBOX_TIMEOUT_TICKS without seeing a peer
+// stops with ST_HANDOFF_TIMEOUT, and its later exchanges only send.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long MBOX_TIMEOUT_TICKS = 3000000000ull;  // 30 s of s_memrealtime (100 MHz)
+__global__ __launch_bounds__(256) void k_exchange(Params P) {
+    const int tid = threadIdx.x;
+    const int G = P.nin;
+    const int nh = P.pr_stride * (int)(sizeof(ArgMinEntry) / 4);  // 32-bit halves per record
+    const uint32_t seq = ld_agent(P.mbox_seq) + 1u;
+    const int64_t par = seq & 1u;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.price_out);
+    for (int k = tid; k < G * nh; k += 256) {
+        const int g = k / nh, h = k - g * nh;
+        const uint64_t w = ((uint64_t)seq << 32) | src[h];
+        __hip_atomic_store(&P.mbox_peer[g][(par * G + P.mbox_rank) * nh + h], w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const bool dead = ld_agent(&P.st->status) == ST_HANDOFF_TIMEOUT;
+    __shared__ int s_to;
+    if (tid == 0) s_to = 0;
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(const_cast<ArgMinEntry*>(P.price_in));
+    const unsigned long long t0 = rtime();
+    for (int k = tid; k < G * nh; k += 256) {
+        const uint64_t* p = &P.mbox[par * G * nh + k];
+        uint64_t w = 0;
+        bool ok = false;
+        while (!dead) {
+            w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((uint32_t)(w >> 32) == seq) {
+                ok = true;
+                break;
+            }
+            if (rtime() - t0 > MBOX_TIMEOUT_TICKS) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) s_to = 1;  // (a benign race: every writer stores 1)
+        dst[k] = (uint32_t)w;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        st_agent(P.mbox_seq, seq);
+        if (s_to) P.st->status = ST_HANDOFF_TIMEOUT;
+    }
+}
+
+hipError_t launch_exchange(const Params& P, hipStream_t s) {
+    hipLaunchKernelGGL(k_exchange, dim3(1), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize_rs(const Params& P, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize_rs, dim3(1), dim3(256), 0, s, P);
     return hipGetLastError();

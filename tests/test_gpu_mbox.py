@@ -1,0 +1,88 @@
+"""GPU: the MINLOC exchange through peer mailboxes (spx_mbox_export /
+spx_mbox_attach, k_exchange) instead of the RCCL all-gather.
+
+- One rank (SPX_FLAG_COMM1, its own mailbox only): eager and captured
+  passes, and the stepping API, bit-identical to the single-rank loop.
+- Two and three processes on ONE GPU (ranks of a column-sharded group that
+  share the device; RCCL refuses two ranks on one device, the mailboxes do
+  not): each rank maps the others' mailboxes over IPC, and every rank reaches
+  the single-rank state bit for bit, then the oracle's optimum.  This runs
+  the multi-process sharded path on hardware: separate processes, separate
+  contexts, candidate records crossing between them every pass."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("window", [-1, 16])
+@pytest.mark.parametrize("graph_batch", [-1, 16])
+def test_mbox_one_rank_matches_single_rank(spx, window, graph_batch):
+    m, n, seed, k = 300, 1200, 3, 150
+    with spx.Context(m=m, n=n, seed=seed, window=window, persist=False) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+        rp = ref.price()
+    with spx.Context(m=m, n=n, seed=seed, window=window, comm1=True, graph_batch=graph_batch) as ctx:
+        ctx.mbox_attach([ctx.mbox_export()])
+        st, piv = ctx.iterate(k)
+        cfg = ctx.config()
+        s = ctx.state(binv=True)
+        p = ctx.price()
+    assert piv == k
+    if graph_batch > 0:  # a plain kernel: the capture never falls back
+        assert cfg["graph_batch"] == (16 if window < 0 else 30)
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(s[key], rs[key]), key
+    assert p == rp
+
+
+def test_mbox_attach_errors(spx):
+    with spx.Context(m=64, n=256, seed=0) as ctx:  # one rank, no COMM1: no exchange at all
+        with pytest.raises(spx.SimplexError, match="nranks > 1"):
+            ctx.mbox_export()
+    with spx.Context(m=64, n=256, seed=0, comm1=True) as ctx:
+        with pytest.raises(spx.SimplexError, match="export first"):
+            ctx.mbox_attach([bytes(64)])
+        with pytest.raises(ValueError):
+            ctx.mbox_attach([b"short"])
+
+
+@pytest.mark.parametrize("G,window,graph_batch", [(2, -1, 16), (2, 16, 16), (2, 64, -1), (3, 16, 16)])
+def test_mbox_processes_share_one_gpu(spx, oracle, tmp_path, G, window, graph_batch):
+    m, n, seed, k = 300, 1200, 3, 120
+    with spx.Context(m=m, n=n, seed=seed, window=window, persist=False) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+        rr = ref.solve()
+    env = dict(os.environ)
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mbox_rank.py"), str(tmp_path), str(g), str(G),
+                               str(m), str(n), str(seed), str(window), str(k), str(graph_batch)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env) for g in range(G)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for g, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {g}:\n{outs[g][-3000:]}"
+    A, b, c = oracle.generate(m, n, seed)
+    o = oracle.solve(A, b, c, eps=1e-7)
+    for g in range(G):
+        r = np.load(tmp_path / f"r{g}.npz")
+        assert int(r["piv"]) == k
+        for key in ("b_ixs", "x_b", "y", "binv"):
+            assert np.array_equal(r[key], rs[key]), (g, key)
+        assert int(r["status"]) == int(spx.SolveStatus.OptimumFound)
+        assert int(r["pivots"]) == rr.pivots == o.pivots
+        assert float(r["z"]) == rr.z
+        assert abs(rr.z - o.z) <= 1e-9 * abs(o.z)
