@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--minloc", choices=["rccl", "mbox"], default="rccl",
                     help="N > 1: the pricing MINLOC exchange as an RCCL all-gather (default) or as direct "
                          "stores into the peers' mailboxes (spx_mbox_attach, one small kernel per pass)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of --gpus N on a one-GPU box: every rank on GPU 0 (gloo process group, "
+                         "mailbox MINLOC; RCCL refuses two ranks on one device). Exercises the multi-rank "
+                         "bench path; its timings are not a scaling measurement")
     a = ap.parse_args()
     m, n = CONFIGS[a.config or "C3"]
     a.m = a.m or m
@@ -118,10 +122,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if args.share_gpu:  # rehearsal: every rank on GPU 0, gloo process group, mailbox MINLOC
+        local = 0
+        args.minloc = "mbox"
     torch.cuda.set_device(local)
     multi = world > 1 or args.comm1  # the multi-rank code path (RCCL exchange)
     if multi:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import simplex_method_gpu_amd as spx
 
     m, n = args.m, args.n
@@ -150,14 +160,14 @@ def main():
     def reduce_max(vals):
         if not multi:
             return list(vals)
-        t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
+        t = torch.tensor(list(vals), dtype=torch.float64, device="cpu" if args.share_gpu else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.tolist()
 
     def reduce_sum(vals):
         if not multi:
             return list(vals)
-        t = torch.tensor(list(vals), dtype=torch.float64, device="cuda")
+        t = torch.tensor(list(vals), dtype=torch.float64, device="cpu" if args.share_gpu else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.tolist()
 
@@ -355,6 +365,9 @@ def main():
             "tableau": tab,
             "cpu_baseline": cpu,
         }
+        if args.share_gpu:
+            out["rehearsal"] = (f"{world} ranks share one GPU (--share-gpu: gloo process group, mailbox MINLOC); "
+                                "checks the multi-rank path, not a scaling number")
         print(json.dumps(out), flush=True)
     if multi:
         dist.destroy_process_group()
