@@ -934,9 +934,11 @@ int reinvert_current(spx_ctx* x) {
 // Window tableau without k_fold (Params::tab_slack): needs A[:, n-m:] = I
 // exactly (the slack basis the reference's init assumes, v4:272-275).
 // A == nullptr: generated [U | I].  SPX_TAB_BW=1 keeps B_w and k_fold.
-bool tab_slack_ok(const double* A, int64_t m, int64_t n) {
-    const char* env = std::getenv("SPX_TAB_BW");
-    if (env && env[0] == '1') return false;
+bool env_on(const char* name) {
+    const char* env = std::getenv(name);
+    return env && env[0] == '1';
+}
+bool slack_identity(const double* A, int64_t m, int64_t n) {
     if (!A) return true;
     for (int64_t i = 0; i < m; ++i) {
         const double* col = A + (n - m + i) * m;  // column-major m x n
@@ -944,6 +946,14 @@ bool tab_slack_ok(const double* A, int64_t m, int64_t n) {
             if (col[r] != (r == i ? 1.0 : 0.0)) return false;
     }
     return true;
+}
+// the two uses of A[:, n-m:] = I (A == nullptr: generated [U | I]): the
+// tableau's B_w from T_w, and k_price's unit slack columns (SPX_DENSE_SLACKS=1:
+// stream them like any column)
+void set_slack_flags(spx_ctx* x, const double* A, int64_t m, int64_t n) {
+    const bool ident = slack_identity(A, m, n);
+    if (x->P.tab) x->P.tab_slack = (ident && !env_on("SPX_TAB_BW")) ? 1 : 0;
+    x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
 }
 
 int create_tail(spx_ctx* x) {
@@ -975,7 +985,7 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
         if (e == hipSuccess) e = hipMemcpy(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK && x->P.tab) x->P.tab_slack = tab_slack_ok(A, m, n) ? 1 : 0;
+    if (rc == SPX_OK) set_slack_flags(x, A, m, n);
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;
@@ -998,7 +1008,7 @@ int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed, con
         hipError_t e = launch_generate(x->A, x->b, x->c, m, n, x->L, seed, x->stream);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "generate failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK && x->P.tab) x->P.tab_slack = tab_slack_ok(nullptr, m, n) ? 1 : 0;  // [U | I] by construction
+    if (rc == SPX_OK) set_slack_flags(x, nullptr, m, n);  // [U | I] by construction
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;

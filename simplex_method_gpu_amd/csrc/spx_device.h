@@ -254,7 +254,9 @@ struct Params {
     uint64_t* mbox;
     uint32_t* mbox_seq;
     int32_t mbox_rank;
-    int32_t pad_mb;
+    // A[:, ns:] = I exactly (checked at create; SPX_DENSE_SLACKS=1 turns it
+    // off): k_price prices a non-basic slack column without streaming it
+    int32_t slack_unit;
 };
 
 __device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {

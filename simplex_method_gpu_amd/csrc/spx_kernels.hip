@@ -336,7 +336,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // The first CH chunks of every column are loaded before the previous
     // column's reduction (and, for the first column, before the LDS fill), so
     // a wave's A stream does not stall at column boundaries.
-    bool have = pre;
+    // slack columns (A[:, ns:] = I, P.slack_unit): the unit vector's dot
+    // products without its stream (see below)
+    auto unit_col = [&](int64_t jj) { return P.slack_unit && jj >= P.ns; };
+    bool have = pre && !unit_col(j0);
     for (int idx = idx0; idx < nlist; idx += stride) {
         const bool first = idx == idx0;
         const int64_t j = first ? j0 : (int64_t)P.nb_list[idx];
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
         double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
         int64_t k = lane;
+        const bool unit = unit_col(j);
         // Two 8-chunk batches in flight through the column: the batch after
         // the prefetched first one is requested before that one is consumed,
         // and every later batch before its predecessor is (kb: the batch
@@ -389,7 +393,25 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             consume(vc, 8, kb);
             k = L2;
         };
-        if (pipe && WIN && pend) {
+        if (unit) {
+            // column ns + i is e_i: every lane partial of the dense sum stays
+            // +0 except the one holding element i, which is fma(1, y_i, +0)
+            // (fma with the exact zeros of the other rows adds +-0), so
+            // these are the dense loop's bits without its 8L-byte stream
+            const int64_t i = j - P.ns, k2 = i >> 1;
+            if (lane == (int)(k2 & 63)) {
+                const dbl2 w = Y(k2);
+                const double v = fma(1.0, (i & 1) ? w.y : w.x, 0.0);
+                if (i & 1) a1 = v;
+                else a0 = v;
+                if (WIN && pend) {
+                    const dbl2 r = Rw(k2);
+                    const double u = fma(1.0, (i & 1) ? r.y : r.x, 0.0);
+                    if (i & 1) b1 = u;
+                    else b0 = u;
+                }
+            }
+        } else if (pipe && WIN && pend) {
             run_pipe(std::true_type());
         } else if (pipe) {
             run_pipe(std::false_type());
@@ -462,9 +484,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         // next column's first chunks in flight during this column's reduction
         const int nidx = idx + stride;
-        have = nidx < nlist && L2 >= CH * 64;
+        const int64_t jn = nidx < nlist ? (int64_t)P.nb_list[nidx] : 0;
+        have = nidx < nlist && L2 >= CH * 64 && !unit_col(jn);
         if (have) {
-            const dbl2* cn = reinterpret_cast<const dbl2*>(P.A + (int64_t)P.nb_list[nidx] * L);
+            const dbl2* cn = reinterpret_cast<const dbl2*>(P.A + jn * L);
 #pragma unroll
             for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&cn[lane + u * 64]);
         }
