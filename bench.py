@@ -214,9 +214,11 @@ def main():
                       "price_minloc_ms": 1e-3 * lt["price_us"], "update_ms": 1e-3 * lt["ftran_us"],
                       "loop_ms_per_pass": lt["loop_ms"] / max(lt["loop_passes"], 1)}
         info1 = ctx.info()
+        cols = ctx.ftran_cols()
         ctx.close()
         return {"cfg": cfg, "dt": dt, "pivots": piv1 - piv0, "steps": steps, "lead": lead, "dispatch": delta,
                 "pt": pt, "lt": lt, "nb": 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"]),
+                "price_bytes": 0.5 * (info0["bytes_price"] + info1["bytes_price"]), "ftran_cols": cols,
                 "status": int(st)}
 
     def kernel_split(run, window):
@@ -226,10 +228,14 @@ def main():
         price_ms = pt["price_ms"] / passes
         minloc_ms = pt["price_minloc_ms"] / passes
         update_ms = pt["update_ms"] / passes
-        price_bytes = 8.0 * (m + 1) * run["nb"]  # this rank's launch
+        # this rank's launch: the streamed non-basic columns
+        # (non-basic slacks are priced without their column, spx_info)
+        price_bytes = run["price_bytes"]
         # B^-1 bytes of the update launch: read + write (explicit rank-1
-        # update), or the read-only FTRAN stream of the eta window
-        update_bytes = (8.0 if window > 0 else 16.0) * m * m
+        # update), or the read-only FTRAN stream of the eta window: its
+        # non-unit columns with the compact operand (spx_ftran_cols, as of the
+        # window's last fold: an upper bound over the window)
+        update_bytes = 8.0 * m * run["ftran_cols"] if window > 0 else 16.0 * m * m
         fold_ms = lt["fold_ms"] / lt["folds"] if lt and lt["folds"] else 0.0
         return {"price_ms": price_ms, "minloc_ms": minloc_ms, "update_ms": update_ms,
                 "price_bytes": price_bytes, "update_bytes": update_bytes, "fold_ms": fold_ms,
@@ -251,8 +257,8 @@ def main():
     update_gbs = ks["update_bytes"] / (ks["update_ms"] * 1e-3) / 1e9 if ks["update_ms"] > 0 else 0.0
     # fold: B_w read + written, U / Qrows read once per window
     fold_bytes = 16.0 * m * m + 8.0 * win * 2 * m if win else 0.0
-    b_upd = 8.0 * m * m * (1.0 + 2.0 / (win - 1)) if win else 16.0 * m * m
-    b_moved = 8.0 * (m + 1) * (n - m) + b_upd            # this representation, per pivot
+    b_upd = 8.0 * m * ev_run["ftran_cols"] + 16.0 * m * m / (win - 1) if win else 16.0 * m * m
+    b_moved = price_bytes_all + b_upd                       # this representation, per pivot
     b_alg = 8.0 * (m + 1) * (n - m) + 16.0 * m * m         # SURVEY.md §8(d) B_alg, per pivot
 
     traffic = None
@@ -399,8 +405,7 @@ def sharded_pricing_block(make, reduce_max, reduce_sum, world, args):
     passes = max(pt["passes"], 1)
     price_ms = pt["price_ms"] / passes
     pm_ms = pt["price_minloc_ms"] / passes
-    nb = 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"])
-    bytes_rank = 8.0 * (m4 + 1) * nb
+    bytes_rank = 0.5 * (info0["bytes_price"] + info1["bytes_price"])  # streamed columns (spx_info)
     price_max, pm_max = reduce_max([price_ms, pm_ms])
     bytes_all = reduce_sum([bytes_rank])[0]
     return {"config": f"C4 m={m4} n={n4}, pricing columns sharded over {world} rank(s)",

@@ -339,6 +339,12 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
 #define SPX_CONFIG_FIELDS 12
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
+/* Columns of B^-1 the FTRAN stream reads per row: m, or with the eta window's
+ * compact operand (A[:, n-m:] = I, two-kernel passes; SPX_DENSE_FTRAN=1 turns
+ * it off) the non-unit columns of B_w as of the last fold: B_w is I except in
+ * the columns of rows whose slack has left the basis. */
+int spx_ftran_cols(spx_ctx* ctx, int32_t* cols);
+
 /* What the loop has enqueued since spx_create (monotone counters, so a
  * caller can difference them around a timed region): out[0] passes launched
  * eagerly (step-wise spx_price/spx_pivot included), [1] captured-hipGraph

@@ -327,6 +327,12 @@ class Context:
                 "bytes_price": bp.value, "bytes_update": bu.value}
 
 
+    def ftran_cols(self) -> int:
+        """Columns of B^-1 per row the FTRAN stream reads (spx_ftran_cols)."""
+        v = ctypes.c_int32()
+        check(self._L.spx_ftran_cols(self._h, ctypes.byref(v)))
+        return v.value
+
     def dispatch_stats(self):
         """Monotone counts of what the loop enqueued (spx_dispatch_stats)."""
         out = (ctypes.c_int64 * 8)()

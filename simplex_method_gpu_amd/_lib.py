@@ -50,6 +50,7 @@ SIGNATURES = {
     "spx_comm_unique_id": (ctypes.c_int, [_p]),
     "spx_attach_comm": (ctypes.c_int, [_p, _p]),
     "spx_mbox_export": (ctypes.c_int, [_p, _p]),
+    "spx_ftran_cols": (ctypes.c_int, [_p, _p]),
     "spx_mbox_attach": (ctypes.c_int, [_p, _p]),
     "spx_reset": (ctypes.c_int, [_p]),
     "spx_reinvert": (ctypes.c_int, [_p]),

@@ -111,6 +111,7 @@ struct spx_ctx {
     uint64_t** mbox_peer = nullptr;  // device array of nranks mailbox pointers
     std::vector<void*> mbox_opened;  // IPC mappings of the other ranks' mailboxes
     bool mbox_ready = false;
+    bool bc_want = false;  // compact FTRAN operand wanted (allocated when A[:, n-m:] = I)
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
 
     // graph replay of `batch` passes
@@ -213,6 +214,8 @@ const char* spx_status_string(int32_t s) {
 namespace {
 
 int reset_stamps(spx_ctx* x);
+
+bool env_on(const char* name);
 
 int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (opts) x->opts = *opts; else spx_default_opts(&x->opts);
@@ -472,6 +475,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
             x->persist = true;
         }
     }
+    // compact FTRAN operand (Params::bc): two-kernel window passes on one
+    // device-resident B_w with A[:, n-m:] = I (checked below, after the
+    // upload), while A_p's gather fits beside the k_update LDS
+    x->bc_want = P.win && !P.tab && !x->persist && !P.row_shard && L * 8 <= 65536 && !env_on("SPX_DENSE_FTRAN");
     if (x->opts.flags & SPX_FLAG_STAMPS) {
         SPX_TRY(x->alloc(&P.stamps, 32));
         SPX_TRY(reset_stamps(x));
@@ -530,6 +537,11 @@ int do_reset(spx_ctx* x) {
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
     HIP_TRY(launch_reset(x->P, x->stream));
+    if (x->P.bc) {  // B_w = I: no column list
+        HIP_TRY(hipMemsetAsync(x->P.rleft, 0, (size_t)x->L * sizeof(int32_t), x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.rmap, 0xFF, (size_t)x->L * sizeof(int32_t), x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, 4 * sizeof(int32_t), x->stream));
+    }
     SPX_TRY(tab_rebuild(x, true));
     HIP_TRY(hipStreamSynchronize(x->stream));
     x->pivots = 0;
@@ -904,6 +916,16 @@ int reinvert_basis(spx_ctx* x, const int64_t* basis) {
         return fail(SPX_ERR_SINGULAR, "singular basis: no pivot above tolerance for column %lld (basis position %lld)",
                     (long long)basis[rs.bad_pos], (long long)rs.bad_pos);
     HIP_TRY(rv_launch_finish(x->P, R, x->rv_Ypart, x->stream));
+    if (x->P.bc) {  // the new B_w's non-unit columns: rows whose slack is not basic in them
+        std::vector<int32_t> left((size_t)x->L, 0);
+        for (int64_t k = 0; k < m; ++k) left[(size_t)k] = basis[k] != ns + k ? 1 : 0;
+        HIP_TRY(hipMemcpyAsync(x->P.rleft, left.data(), (size_t)x->L * sizeof(int32_t), hipMemcpyHostToDevice,
+                               x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.rmap, 0xFF, (size_t)x->L * sizeof(int32_t), x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, 4 * sizeof(int32_t), x->stream));
+        HIP_TRY(launch_compact(x->P, x->stream));
+        HIP_TRY(hipStreamSynchronize(x->stream));  // (left is a host buffer)
+    }
     SPX_TRY(tab_rebuild(x, false));
     x->nw = 0;
     return read_state(x);
@@ -950,10 +972,19 @@ bool slack_identity(const double* A, int64_t m, int64_t n) {
 // the two uses of A[:, n-m:] = I (A == nullptr: generated [U | I]): the
 // tableau's B_w from T_w, and k_price's unit slack columns (SPX_DENSE_SLACKS=1:
 // stream them like any column)
-void set_slack_flags(spx_ctx* x, const double* A, int64_t m, int64_t n) {
+int set_slack_flags(spx_ctx* x, const double* A, int64_t m, int64_t n) {
     const bool ident = slack_identity(A, m, n);
     if (x->P.tab) x->P.tab_slack = (ident && !env_on("SPX_TAB_BW")) ? 1 : 0;
     x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
+    if (x->bc_want && ident) {  // compact FTRAN operand (do_reset initialises it)
+        Params& P = x->P;
+        SPX_TRY(x->alloc(&P.bc, (size_t)(m * x->L)));
+        SPX_TRY(x->alloc(&P.rlist, (size_t)x->L));
+        SPX_TRY(x->alloc(&P.rmap, (size_t)x->L));
+        SPX_TRY(x->alloc(&P.rleft, (size_t)x->L));
+        SPX_TRY(x->alloc(&P.bc_n, 4));
+    }
+    return SPX_OK;
 }
 
 int create_tail(spx_ctx* x) {
@@ -985,7 +1016,7 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
         if (e == hipSuccess) e = hipMemcpy(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK) set_slack_flags(x, A, m, n);
+    if (rc == SPX_OK) rc = set_slack_flags(x, A, m, n);
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;
@@ -1008,7 +1039,7 @@ int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed, con
         hipError_t e = launch_generate(x->A, x->b, x->c, m, n, x->L, seed, x->stream);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "generate failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK) set_slack_flags(x, nullptr, m, n);  // [U | I] by construction
+    if (rc == SPX_OK) rc = set_slack_flags(x, nullptr, m, n);  // [U | I] by construction
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;
@@ -1548,11 +1579,34 @@ int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb,
     if (n) *n = x->n;
     if (ld) *ld = x->L;
     if (local_nb) *local_nb = x->st_host->nb_count;
-    if (bp) *bp = 8.0 * (double)(x->m + 1) * (double)x->st_host->nb_count;
-    // update bytes per pivot: B^-1 read + write, or (eta window) B_w read plus
-    // the fold's read + write spread over its KW-1 pivots
-    if (bu) *bu = x->P.win ? 8.0 * (double)x->m * (double)x->m * (1.0 + 2.0 / (x->P.win - 1))
-                           : 16.0 * (double)x->m * (double)x->m;
+    // pricing bytes: the streamed non-basic columns (with P.slack_unit the
+    // non-basic slacks of this rank's block are priced without their column)
+    int64_t streamed = x->st_host->nb_count;
+    if (x->P.slack_unit) {
+        std::vector<int64_t> bix((size_t)x->m);
+        HIP_TRY(hipMemcpy(bix.data(), x->P.b_ixs, (size_t)x->m * sizeof(int64_t), hipMemcpyDeviceToHost));
+        int64_t basic_slacks = 0;
+        for (int64_t j : bix) basic_slacks += (j >= x->P.k_lo && j < x->P.k_hi) ? 1 : 0;
+        streamed -= (x->P.k_hi - x->P.k_lo) - basic_slacks;
+    }
+    if (bp) *bp = 8.0 * (double)(x->m + 1) * (double)streamed;
+    // update bytes per pivot: B^-1 read + write, or (eta window) the B_w
+    // FTRAN stream (its non-unit columns with the compact operand) plus the
+    // fold's read + write spread over its KW-1 pivots
+    int32_t cols = 0;
+    SPX_TRY(spx_ftran_cols(x, &cols));
+    const double md = (double)x->m;
+    if (bu) *bu = x->P.win ? 8.0 * md * (double)cols + 16.0 * md * md / (x->P.win - 1) : 16.0 * md * md;
+    return SPX_OK;
+}
+
+int spx_ftran_cols(spx_ctx* x, int32_t* cols) {
+    if (!x || !cols) return fail(SPX_ERR_ARG, "NULL argument");
+    *cols = (int32_t)x->m;
+    if (x->P.win && x->P.bc) {
+        HIP_TRY(hipStreamSynchronize(x->stream));
+        HIP_TRY(hipMemcpy(cols, x->P.bc_n, sizeof(int32_t), hipMemcpyDeviceToHost));
+    }
     return SPX_OK;
 }
 

@@ -257,6 +257,20 @@ struct Params {
     // A[:, ns:] = I exactly (checked at create; SPX_DENSE_SLACKS=1 turns it
     // off): k_price prices a non-basic slack column without streaming it
     int32_t slack_unit;
+    int32_t pad_bc;
+    // B_w by its non-unit columns (eta window, two-kernel passes; DESIGN.md
+    // §4a "compact FTRAN").  With A[:, ns:] = I, column k of B_w is e_k while
+    // slack k has stayed basic in row k, so B_w = I + (columns rlist[0..S)).
+    // bc: m x L, row i's first S entries = B_w[i][rlist[c]] (gathered after
+    // every fold from the dense B_w, which stays the master copy); rmap[k] =
+    // c or -1 (unit column); rleft[k] = 1 once row k has been a leaving row
+    // (or, after a reinversion, when slack k is not basic in row k): a
+    // superset of the non-unit columns; bc_n[0] = S.  nullptr: dense FTRAN.
+    double* bc;
+    int32_t* rlist;
+    int32_t* rmap;
+    int32_t* rleft;
+    int32_t* bc_n;
 };
 
 __device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {

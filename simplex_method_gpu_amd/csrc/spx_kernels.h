@@ -30,6 +30,7 @@ hipError_t launch_reset(const Params& P, hipStream_t s);
 hipError_t launch_flush(const Params& P, hipStream_t s);
 hipError_t launch_finalize_rs(const Params& P, hipStream_t s);
 hipError_t launch_exchange(const Params& P, hipStream_t s);
+hipError_t launch_compact(const Params& P, hipStream_t s);
 hipError_t launch_tail(const Params& P, int nparts, hipStream_t s);
 hipError_t launch_materialize(const Params& P, double* out, hipStream_t s);
 hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s);

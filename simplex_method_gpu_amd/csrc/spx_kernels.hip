@@ -58,6 +58,11 @@ namespace spx {
 #define SPX_WIN_U1 8  // eta-window FTRAN stream, 1 row per wave: dbl2 loads per lane per round trip
 #endif
 bool kernels_inplace() { return SPX_INPLACE != 0; }
+// compact FTRAN (Params::bc): dbl2 chunks of each compact row requested at
+// k_update entry (256 columns), and column-list entries per thread requested
+// ahead of the entering column (1,024 columns at 512 threads)
+constexpr int BC_PF = 2;
+constexpr int BC_RL = 2;
 
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
 // launch, slot[1] += (last-workgroup ticket - start), slot[2] += tail duration.
@@ -881,6 +886,7 @@ __device__ __forceinline__ void pivot_bookkeeping(const Params& P, DevState* st,
                                                   int64_t it, const TailPre* pre = nullptr) {
     P.c_B[q] = pre ? pre->c_p : P.c[p];
     P.b_ixs[q] = p;
+    if (P.rleft) P.rleft[q] = 1;  // column q of B^-1 may stop being e_q
     int cnt = pre ? pre->cnt : st->nb_count;
     if (owns_col(P, p)) {
         const int kp = pre ? pre->kp : P.nb_pos[p];
@@ -1006,7 +1012,7 @@ __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2*
     }
 }
 
-template <int BLOCK, int R, bool RS, bool WIN, int BNT>
+template <int BLOCK, int R, bool RS, bool WIN, int BNT, bool BC>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
     using Lds = UpdLds<BLOCK>;
@@ -1036,16 +1042,34 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     constexpr int PFU = WIN ? ((R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2))) : ((R >= 4) ? 2 : 4);
     dbl2 pfb[PFU][R];
     const int64_t pf_row = ((int64_t)blockIdx.x * WAVES + wave) * R;
-    const bool pf_ok = WIN && !RS && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
+    const bool pf_ok = WIN && !RS && !BC && pf_row + R <= P.m && (P.L >> 1) >= PFU * 64;
     if constexpr (WIN && !RS) {
         const int64_t L2c = P.L >> 1;
+        // (compact FTRAN, P.bc: the first BC_PF chunks of this wave's
+        // compact rows, the later ones re-requesting chunk 0 (cache hits), so
+        // the loads stay unconditional and the waits below exact)
         const int64_t prow = pf_row + R <= P.m ? pf_row : (P.m >= R ? P.m - R : 0);
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.B0) + prow * L2c;
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? P.bc : P.B0) + prow * L2c;
 #pragma unroll
         for (int t = 0; t < PFU; ++t) {
-            const int64_t k = lane + t * 64 < L2c ? lane + t * 64 : L2c - 1;
+            const int64_t k = (BC && t >= BC_PF) ? lane : (lane + t * 64 < L2c ? lane + t * 64 : L2c - 1);
 #pragma unroll
             for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * L2c + k]);
+        }
+    }
+    // compact FTRAN: the column list and this wave's unit flags, ahead of p
+    int32_t rlv[BC_RL];
+    int32_t rmv[R];
+    if constexpr (BC) {
+#pragma unroll
+        for (int j = 0; j < BC_RL; ++j) {
+            const int64_t c = tid + (int64_t)j * BLOCK;
+            rlv[j] = P.rlist[c < P.m ? c : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const int64_t i = pf_row + u;
+            rmv[u] = P.rmap[i < P.m ? i : 0];
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1238,6 +1262,60 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             for (int64_t kk = tid; kk < L2; kk += BLOCK) d[kk] = ap[kk];
             __syncthreads();
         }
+        if constexpr (BC) {
+            // compact FTRAN: B_w[i,:].A_p = sum_c bc[i][c] A_p[rlist[c]] (+ A_p[i]
+            // when column i is e_i).  Per lane: the unit term first (lane 0),
+            // then its dbl2 chunks lane + 64 t ascending, .x before .y: one
+            // order for every geometry and dispatch.  A_p gathered onto the
+            // list in LDS; the first BC_PF chunks of each row were requested at
+            // kernel entry (pfb), the rest here.
+            double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
+            const int S = P.bc_n[0];
+            const double* apd = P.A + p * L;
+#pragma unroll
+            for (int j = 0; j < BC_RL; ++j) {
+                const int c = tid + j * BLOCK;
+                if (c < S) apc[c] = apd[rlv[j]];
+            }
+            for (int c = tid + BC_RL * BLOCK; c < S; c += BLOCK) apc[c] = apd[P.rlist[c]];
+            double au[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) au[u] = (u < nvalid && lane == 0 && rmv[u] < 0) ? apd[lr0 + u] : 0.0;
+            lds_barrier();
+            const int S2 = (S + 1) >> 1;  // dbl2 chunks (bc rows are zero past S: gathered only there)
+            const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (u < nvalid) {
+                    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * L2;
+                    double a = au[u];
+                    auto take = [&](dbl2 v, int k2) {
+                        const dbl2 w = apc2[k2];
+                        if (2 * k2 < S) a = fma(v.x, w.x, a);
+                        if (2 * k2 + 1 < S) a = fma(v.y, w.y, a);
+                    };
+#pragma unroll
+                    for (int t = 0; t < BC_PF; ++t) {
+                        const int k2 = lane + 64 * t;
+                        if (k2 < S2) take(pfb[t][u], k2);
+                    }
+                    for (int k0 = BC_PF * 64; k0 < S2; k0 += 8 * 64) {
+                        dbl2 v[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            const int k2 = k0 + lane + 64 * t;
+                            v[t] = brow[k2 < S2 ? k2 : 0];
+                        }
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            const int k2 = k0 + lane + 64 * t;
+                            if (k2 < S2) take(v[t], k2);
+                        }
+                    }
+                    acc[u] = a;
+                }
+            }
+        } else {
         if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
             constexpr int U = (R == 1) ? SPX_WIN_U1 : ((R == 2) ? 8 : ((R == 4) ? 4 : 2));
@@ -1256,6 +1334,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                     acc[u] = fma(bv.y, av.y, acc[u]);
                 }
             }
+        }
         }
 #pragma unroll
         for (int u = 0; u < R; ++u) {
@@ -2072,24 +2151,25 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
     return hipErrorInvalidValue;
 }
 
-template <int BLOCK, int R, bool RS, bool WIN, int BNT = 1>
+template <int BLOCK, int R, bool RS, bool WIN, int BNT = 1, bool BC = false>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const size_t lds = UpdLds<BLOCK>::bytes + ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0) +
+    const size_t lds = UpdLds<BLOCK>::bytes +
+                       ((WIN && (P.bc || (SPX_WIN_APLDS && P.L * 8 <= 65536))) ? (size_t)P.L * 8 : 0) +
                        ((!WIN && !RS && upd_xlds(P)) ? (size_t)P.L * 24 : 0);
     if (lds > 65536) {  // once per instantiation (idempotent; not a stream operation)
         static bool raised = false;
         if (!raised) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_update<BLOCK, R, RS, WIN, BNT>),
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_update<BLOCK, R, RS, WIN, BNT, BC>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
             if (e != hipSuccess) return e;
             raised = true;
         }
     }
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
+        hipExtLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT, BC>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0,
                               P);
     } else {
-        hipLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_update<BLOCK, R, RS, WIN, BNT, BC>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
     return hipGetLastError();
 }
@@ -2100,6 +2180,7 @@ static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipE
     if (!P.win) return launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
     // B_w loads: default policy while B_w fits the Infinity Cache beside the
     // window state (spx_common.h SPX_NT_BWIN), non-temporal beyond
+    if (P.bc) return launch_update_k<BLOCK, R, false, true, 0, true>(P, grid, s, e0, e1);  // compact FTRAN
     if (win_b_cached(P)) return launch_update_k<BLOCK, R, false, true, 0>(P, grid, s, e0, e1);
     return launch_update_k<BLOCK, R, false, true, 1>(P, grid, s, e0, e1);
 }
@@ -2122,11 +2203,64 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
         case 64: hipLaunchKernelGGL(k_fold<64>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_compact(P, s);  // the compact FTRAN operand follows B_w
 }
 
 hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
     hipLaunchKernelGGL(k_tail, dim3(1), dim3(1024), 0, s, P, nparts);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Compact FTRAN operand (Params::bc): after every fold (and reset or
+// reinversion) the rows that have left join the column list in ascending
+// order (k_bc_list, one workgroup), then every row of B_w is gathered onto
+// those columns (k_bc_gather).  The dense B_w stays the master copy.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_bc_list(Params P) {
+    __shared__ int s_w[16];
+    __shared__ int s_base;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_base = P.bc_n[0];
+    __syncthreads();
+    for (int64_t k0 = 0; k0 < P.m; k0 += 1024) {
+        const int64_t k = k0 + tid;
+        const bool nu = k < P.m && P.rleft[k] != 0 && P.rmap[k] < 0;
+        const uint64_t bal = __ballot(nu);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) s_w[wave] = __popcll(bal);
+        __syncthreads();
+        int off = s_base, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            if (w < wave) off += s_w[w];
+            tot += s_w[w];
+        }
+        if (nu) {
+            P.rmap[k] = off + pre;
+            P.rlist[off + pre] = (int32_t)k;
+        }
+        __syncthreads();
+        if (tid == 0) s_base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) P.bc_n[0] = s_base;
+}
+constexpr int BC_ROWS = 4;  // rows per k_bc_gather workgroup
+__global__ __launch_bounds__(256) void k_bc_gather(Params P) {
+    const int S = P.bc_n[0];
+    const int64_t L = P.L;
+    for (int r = 0; r < BC_ROWS; ++r) {
+        const int64_t i = (int64_t)blockIdx.x * BC_ROWS + r;
+        if (i >= P.m) break;
+        for (int c = threadIdx.x; c < S; c += 256) P.bc[i * L + c] = P.B0[i * L + P.rlist[c]];
+    }
+}
+hipError_t launch_compact(const Params& P, hipStream_t s) {
+    if (!P.bc) return hipSuccess;
+    hipLaunchKernelGGL(k_bc_list, dim3(1), dim3(1024), 0, s, P);
+    hipLaunchKernelGGL(k_bc_gather, dim3((unsigned)((P.m + BC_ROWS - 1) / BC_ROWS)), dim3(256), 0, s, P);
     return hipGetLastError();
 }
 

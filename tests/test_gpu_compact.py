@@ -1,0 +1,95 @@
+"""GPU: the compact FTRAN operand (Params::bc: B_w stored by its non-unit
+columns, gathered after every fold) against the dense B_w stream
+(SPX_DENSE_FTRAN=1).  The two sum B_w[i,:].A_p in different orders, so they
+agree within rounding: the same pivot path, states within 1e-10, the same
+optimum.  Within the compact form every dispatch and geometry gives the
+same bits."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _run(spx, dense, k, **kw):
+    with _env(SPX_DENSE_FTRAN="1" if dense else "0"):
+        with spx.Context(trace=4096, **kw) as ctx:
+            st, piv = ctx.iterate(k)
+            s = ctx.state(binv=True)
+            tr = ctx.trace()
+            r = ctx.solve()
+            return piv, s, tr, r
+
+
+def _close(a, b, tol=1e-10):
+    return np.max(np.abs(a - b)) <= tol * max(1.0, np.max(np.abs(b)))
+
+
+@pytest.mark.parametrize("window,m,n,seed,k", [(16, 300, 1200, 5, 200), (64, 512, 2048, 1, 400),
+                                               (64, 1024, 4096, 0, 300), (32, 256, 1024, 7, 250)])
+def test_compact_matches_dense_ftran(spx, window, m, n, seed, k):
+    a = _run(spx, False, k, m=m, n=n, seed=seed, window=window, persist=False)
+    d = _run(spx, True, k, m=m, n=n, seed=seed, window=window, persist=False)
+    assert a[0] == d[0] == k
+    assert np.array_equal(a[1]["b_ixs"], d[1]["b_ixs"])
+    assert np.array_equal(a[2], d[2])  # the same (p, q) per pivot
+    for key in ("x_b", "y", "binv"):
+        assert _close(a[1][key], d[1][key]), key
+    assert a[3].status == d[3].status and a[3].pivots == d[3].pivots
+    assert abs(a[3].z - d[3].z) <= 1e-9 * abs(d[3].z)
+
+
+@pytest.mark.parametrize("kw", [dict(graph_batch=-1), dict(update_rows=2), dict(update_block=256),
+                                dict(refactor_every=100)], ids=["eager", "rows2", "block256", "reinvert"])
+def test_compact_same_bits_every_dispatch(spx, kw):
+    base = dict(m=400, n=1600, seed=2, window=16, persist=False)
+    ref = _run(spx, False, 300, **base)
+    got = _run(spx, False, 300, **base, **kw)
+    if "refactor_every" in kw:  # a reinverted B_w has its own bits: same path, close values
+        assert np.array_equal(got[1]["b_ixs"], ref[1]["b_ixs"])
+        assert _close(got[1]["x_b"], ref[1]["x_b"], 1e-9)
+        assert got[3].pivots == ref[3].pivots and abs(got[3].z - ref[3].z) <= 1e-9 * abs(ref[3].z)
+        return
+    for key in ("b_ixs", "x_b", "binv"):
+        assert np.array_equal(got[1][key], ref[1][key]), key
+    if "update_rows" in kw:
+        # two rows per wave group the ratio-test sum T = sum c_B alpha (and so
+        # s_y, y) differently, with the dense B_w stream as well
+        assert _close(got[1]["y"], ref[1]["y"], 1e-12)
+        assert got[3].pivots == ref[3].pivots and abs(got[3].z - ref[3].z) <= 1e-12 * abs(ref[3].z)
+    else:
+        assert np.array_equal(got[1]["y"], ref[1]["y"])
+        assert got[3].pivots == ref[3].pivots and got[3].z == ref[3].z
+
+
+def test_compact_set_basis_and_oracle(spx, oracle):
+    """Warm start (reinversion builds the column list from the basis), then
+    the solve reaches the oracle's optimum."""
+    m, n, seed = 300, 1200, 9
+    A, b, c = oracle.generate(m, n, seed)
+    o = oracle.solve(A, b, c, eps=1e-7)
+    with spx.Context(A, b, c, window=16, persist=False) as ctx:
+        ctx.iterate(150)
+        basis = ctx.state()["b_ixs"].copy()
+    with spx.Context(A, b, c, window=16, persist=False) as ctx:
+        ctx.set_basis(basis)
+        r = ctx.solve()
+    assert r.status == spx.SolveStatus.OptimumFound
+    assert abs(r.z - o.z) <= 1e-9 * abs(o.z)
