@@ -62,6 +62,7 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 // k_update entry (256 columns), and column-list entries per thread requested
 // ahead of the entering column (1,024 columns at 512 threads)
 constexpr int BC_PF = 2;
+constexpr int BC_PF2 = 4;  // chunks requested once S is known (up to 512 columns)
 constexpr int BC_RL = 2;
 
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
@@ -1158,6 +1159,32 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         return;
     }
 
+    // compact FTRAN (BC): with p known, the operands that depend on it or on
+    // S are requested now, ahead of the row scalars (vmcnt retires in order):
+    // this row's chunks BC_PF..BC_PF2-1 (chunks past S re-request chunk 0, a
+    // cache hit, so the loads stay unconditional), A_p on the column list
+    // and A_p[i] for the unit term
+    int Sbc = 0;
+    dbl2 pf2[BC_PF2 - BC_PF][R];
+    double apv[BC_RL], auv[R];
+    if constexpr (BC) {
+        Sbc = P.bc_n[0];
+        const int64_t L2c = P.L >> 1;
+        const int64_t prow = pf_row + R <= P.m ? pf_row : (P.m >= R ? P.m - R : 0);
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.bc) + prow * L2c;
+#pragma unroll
+        for (int t = BC_PF; t < BC_PF2; ++t) {
+            const int k2 = lane + 64 * t;
+            const int kk = (2 * k2 < Sbc && k2 < L2c) ? k2 : lane;
+#pragma unroll
+            for (int u = 0; u < R; ++u) pf2[t - BC_PF][u] = b0[u * L2c + kk];
+        }
+        const double* apd = P.A + p * P.L;
+#pragma unroll
+        for (int j = 0; j < BC_RL; ++j) apv[j] = apd[rlv[j]];
+#pragma unroll
+        for (int u = 0; u < R; ++u) auv[u] = apd[prow + u];
+    }
     const int64_t it = Sv.iter;
     const int par = (int)(it & 1);
     const int64_t m = P.m, L = P.L, L2 = L >> 1;
@@ -1270,17 +1297,17 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             // list in LDS; the first BC_PF chunks of each row were requested at
             // kernel entry (pfb), the rest here.
             double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
-            const int S = P.bc_n[0];
+            const int S = Sbc;
             const double* apd = P.A + p * L;
 #pragma unroll
             for (int j = 0; j < BC_RL; ++j) {
                 const int c = tid + j * BLOCK;
-                if (c < S) apc[c] = apd[rlv[j]];
+                if (c < S) apc[c] = apv[j];
             }
             for (int c = tid + BC_RL * BLOCK; c < S; c += BLOCK) apc[c] = apd[P.rlist[c]];
             double au[R];
 #pragma unroll
-            for (int u = 0; u < R; ++u) au[u] = (u < nvalid && lane == 0 && rmv[u] < 0) ? apd[lr0 + u] : 0.0;
+            for (int u = 0; u < R; ++u) au[u] = (u < nvalid && lane == 0 && rmv[u] < 0) ? auv[u] : 0.0;
             lds_barrier();
             const int S2 = (S + 1) >> 1;  // dbl2 chunks (bc rows are zero past S: gathered only there)
             const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
@@ -1299,7 +1326,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
                         const int k2 = lane + 64 * t;
                         if (k2 < S2) take(pfb[t][u], k2);
                     }
-                    for (int k0 = BC_PF * 64; k0 < S2; k0 += 8 * 64) {
+#pragma unroll
+                    for (int t = BC_PF; t < BC_PF2; ++t) {
+                        const int k2 = lane + 64 * t;
+                        if (k2 < S2) take(pf2[t - BC_PF][u], k2);
+                    }
+                    for (int k0 = BC_PF2 * 64; k0 < S2; k0 += 8 * 64) {
                         dbl2 v[8];
 #pragma unroll
                         for (int t = 0; t < 8; ++t) {
