@@ -289,7 +289,10 @@ def main():
         cpu["glpk"] = glpk_status()
 
     if rank == 0:
-        rep = ("eta window %d: B_w + U R, FTRAN stream read-only, rank-%d fold every %d pivots" % (win, win - 1, win - 1)
+        fc = ev_run["ftran_cols"]
+        rep = (("eta window %d: B_w + U R, FTRAN stream read-only, rank-%d fold every %d pivots" % (win, win - 1, win - 1)
+                + ("; B_w's non-unit columns only (compact FTRAN operand, %d of %d columns at the window's end)"
+                   % (fc, m) if fc < m else ""))
                if win else "explicit B^-1, rank-1 update in place every pivot (v4:331-333)")
         out = {
             "metric": METRIC.format(m=m, n=n),
