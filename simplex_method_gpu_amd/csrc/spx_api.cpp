@@ -111,7 +111,8 @@ struct spx_ctx {
     uint64_t** mbox_peer = nullptr;  // device array of nranks mailbox pointers
     std::vector<void*> mbox_opened;  // IPC mappings of the other ranks' mailboxes
     bool mbox_ready = false;
-    bool bc_want = false;  // compact FTRAN operand wanted (allocated when A[:, n-m:] = I)
+    bool bc_want = false;      // compact FTRAN operand wanted (allocated by set_slack_flags)
+    bool slack_ident = false;  // A[:, n-m:] = I (checked before setup_common)
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
 
     // graph replay of `batch` passes
@@ -216,6 +217,11 @@ namespace {
 int reset_stamps(spx_ctx* x);
 
 bool env_on(const char* name);
+// the compact FTRAN operand applies: eta window (no tableau, replicated
+// storage) and A[:, n-m:] = I (x->slack_ident, known before setup)
+bool bc_possible(const spx_ctx* x, const Params& P) {
+    return P.win && !P.tab && !P.row_shard && x->slack_ident && !env_on("SPX_DENSE_FTRAN");
+}
 
 int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (opts) x->opts = *opts; else spx_default_opts(&x->opts);
@@ -444,6 +450,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         // measured (tools/loop_sweep.sh): the persistent loop wins once the
         // base row is read from L2 (C5: 729 vs 681 it/s) and loses at C3
         // (8.3k vs 9.3k it/s), so by default only then
+        // (the compact FTRAN operand does not change this: at C5 its two-kernel
+        // pass ran 700 it/s, pricing with the base row from L2 1,384 us, against
+        // the dense persistent loop's 740; tools/r02_c5compact.sh)
         const bool want = (x->opts.flags & SPX_FLAG_PERSIST) || !x->lcfg.lds_r;
         if (x->lcfg.ok && want) {
             SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
@@ -478,7 +487,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // compact FTRAN operand (Params::bc): two-kernel window passes on one
     // device-resident B_w with A[:, n-m:] = I (checked below, after the
     // upload), while A_p's gather fits beside the k_update LDS
-    x->bc_want = P.win && !P.tab && !x->persist && !P.row_shard && L * 8 <= 65536 && !env_on("SPX_DENSE_FTRAN");
+    x->bc_want = bc_possible(x, P) && !x->persist;
     if (x->opts.flags & SPX_FLAG_STAMPS) {
         SPX_TRY(x->alloc(&P.stamps, 32));
         SPX_TRY(reset_stamps(x));
@@ -972,8 +981,9 @@ bool slack_identity(const double* A, int64_t m, int64_t n) {
 // the two uses of A[:, n-m:] = I (A == nullptr: generated [U | I]): the
 // tableau's B_w from T_w, and k_price's unit slack columns (SPX_DENSE_SLACKS=1:
 // stream them like any column)
-int set_slack_flags(spx_ctx* x, const double* A, int64_t m, int64_t n) {
-    const bool ident = slack_identity(A, m, n);
+int set_slack_flags(spx_ctx* x) {
+    const bool ident = x->slack_ident;
+    const int64_t m = x->m;
     if (x->P.tab) x->P.tab_slack = (ident && !env_on("SPX_TAB_BW")) ? 1 : 0;
     x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
     if (x->bc_want && ident) {  // compact FTRAN operand (do_reset initialises it)
@@ -1006,6 +1016,7 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
     if (n > (int64_t)0x7fffffff) return fail(SPX_ERR_ARG, "n too large");
     if (!A || !b || !c) return fail(SPX_ERR_ARG, "NULL input array");
     spx_ctx* x = new spx_ctx();
+    x->slack_ident = slack_identity(A, m, n);
     int rc = setup_common(x, m, n, opts);
     if (rc == SPX_OK) {
         // blocking copies from pageable memory, after the zero-fills queued on the stream
@@ -1016,7 +1027,7 @@ int spx_create(spx_ctx** out, int64_t m, int64_t n, const double* A, const doubl
         if (e == hipSuccess) e = hipMemcpy(x->c, c, (size_t)n * 8, hipMemcpyHostToDevice);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK) rc = set_slack_flags(x, A, m, n);
+    if (rc == SPX_OK) rc = set_slack_flags(x);
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;
@@ -1034,12 +1045,13 @@ int spx_create_generated(spx_ctx** out, int64_t m, int64_t n, uint64_t seed, con
     if (m <= 0 || n < m) return fail(SPX_ERR_ARG, "m must be in [1, n] (m=%lld n=%lld)", (long long)m, (long long)n);
     if (n > (int64_t)0x7fffffff) return fail(SPX_ERR_ARG, "n too large");
     spx_ctx* x = new spx_ctx();
+    x->slack_ident = true;  // [U | I] by construction
     int rc = setup_common(x, m, n, opts);
     if (rc == SPX_OK) {
         hipError_t e = launch_generate(x->A, x->b, x->c, m, n, x->L, seed, x->stream);
         if (e != hipSuccess) rc = fail(SPX_ERR_HIP, "generate failed: %s", hipGetErrorString(e));
     }
-    if (rc == SPX_OK) rc = set_slack_flags(x, nullptr, m, n);  // [U | I] by construction
+    if (rc == SPX_OK) rc = set_slack_flags(x);
     if (rc == SPX_OK) rc = create_tail(x);
     if (rc != SPX_OK) {
         std::string keep = g_err;

@@ -63,6 +63,7 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 // ahead of the entering column (1,024 columns at 512 threads)
 constexpr int BC_PF = 2;
 constexpr int BC_PF2 = 4;  // chunks requested once S is known (up to 512 columns)
+constexpr int BC_APC = 8192;  // A_p gathered onto the list in LDS blocks of this many columns
 constexpr int BC_RL = 2;
 
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
@@ -1299,54 +1300,64 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
             const int S = Sbc;
             const double* apd = P.A + p * L;
-#pragma unroll
-            for (int j = 0; j < BC_RL; ++j) {
-                const int c = tid + j * BLOCK;
-                if (c < S) apc[c] = apv[j];
-            }
-            for (int c = tid + BC_RL * BLOCK; c < S; c += BLOCK) apc[c] = apd[P.rlist[c]];
-            double au[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u) au[u] = (u < nvalid && lane == 0 && rmv[u] < 0) ? auv[u] : 0.0;
-            lds_barrier();
-            const int S2 = (S + 1) >> 1;  // dbl2 chunks (bc rows are zero past S: gathered only there)
+            const int S2 = (S + 1) >> 1;  // dbl2 chunks
             const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
+            double a[R];
 #pragma unroll
-            for (int u = 0; u < R; ++u) {
-                if (u < nvalid) {
-                    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * L2;
-                    double a = au[u];
-                    auto take = [&](dbl2 v, int k2) {
-                        const dbl2 w = apc2[k2];
-                        if (2 * k2 < S) a = fma(v.x, w.x, a);
-                        if (2 * k2 + 1 < S) a = fma(v.y, w.y, a);
-                    };
+            for (int u = 0; u < R; ++u) a[u] = (u < nvalid && lane == 0 && rmv[u] < 0) ? auv[u] : 0.0;
+            // column blocks of BC_APC (one at S <= 8192): A_p on the block's
+            // list entries into LDS, then every row's chunks of the block
+            for (int cb = 0; cb < S || cb == 0; cb += BC_APC) {
+                const int ce = S < cb + BC_APC ? S : cb + BC_APC;
+                if (cb > 0) lds_barrier();  // the previous block's reads are done
 #pragma unroll
-                    for (int t = 0; t < BC_PF; ++t) {
-                        const int k2 = lane + 64 * t;
-                        if (k2 < S2) take(pfb[t][u], k2);
-                    }
+                for (int j = 0; j < BC_RL; ++j) {
+                    const int c = tid + j * BLOCK;
+                    if (cb == 0 && c < ce) apc[c] = apv[j];
+                }
+                for (int c = cb + (cb == 0 ? BC_RL * BLOCK : 0) + tid; c < ce; c += BLOCK) apc[c - cb] = apd[P.rlist[c]];
+                lds_barrier();
+                const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
 #pragma unroll
-                    for (int t = BC_PF; t < BC_PF2; ++t) {
-                        const int k2 = lane + 64 * t;
-                        if (k2 < S2) take(pf2[t - BC_PF][u], k2);
-                    }
-                    for (int k0 = BC_PF2 * 64; k0 < S2; k0 += 8 * 64) {
-                        dbl2 v[8];
+                for (int u = 0; u < R; ++u) {
+                    if (u < nvalid) {
+                        const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * L2;
+                        auto take = [&](dbl2 v, int k2) {
+                            const dbl2 w = apc2[k2 - kb];
+                            if (2 * k2 < S) a[u] = fma(v.x, w.x, a[u]);
+                            if (2 * k2 + 1 < S) a[u] = fma(v.y, w.y, a[u]);
+                        };
+                        if (cb == 0) {
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) {
-                            const int k2 = k0 + lane + 64 * t;
-                            v[t] = brow[k2 < S2 ? k2 : 0];
+                            for (int t = 0; t < BC_PF; ++t) {
+                                const int k2 = lane + 64 * t;
+                                if (k2 < ke) take(pfb[t][u], k2);
+                            }
+#pragma unroll
+                            for (int t = BC_PF; t < BC_PF2; ++t) {
+                                const int k2 = lane + 64 * t;
+                                if (k2 < ke) take(pf2[t - BC_PF][u], k2);
+                            }
                         }
+                        for (int k0 = (cb == 0 ? BC_PF2 * 64 : kb); k0 < ke; k0 += 8 * 64) {
+                            dbl2 v[8];
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) {
-                            const int k2 = k0 + lane + 64 * t;
-                            if (k2 < S2) take(v[t], k2);
+                            for (int t = 0; t < 8; ++t) {
+                                const int k2 = k0 + lane + 64 * t;
+                                v[t] = brow[k2 < ke ? k2 : kb];
+                            }
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int k2 = k0 + lane + 64 * t;
+                                if (k2 < ke) take(v[t], k2);
+                            }
                         }
                     }
-                    acc[u] = a;
                 }
             }
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (u < nvalid) acc[u] = a[u];
         } else {
         if (nvalid == R) {
             // 16 dbl2 loads of B per lane in flight: a 32 KiB row is two round trips
@@ -2186,7 +2197,8 @@ hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEv
 template <int BLOCK, int R, bool RS, bool WIN, int BNT = 1, bool BC = false>
 static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = UpdLds<BLOCK>::bytes +
-                       ((WIN && (P.bc || (SPX_WIN_APLDS && P.L * 8 <= 65536))) ? (size_t)P.L * 8 : 0) +
+                       ((WIN && BC) ? (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8
+                                    : ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0)) +
                        ((!WIN && !RS && upd_xlds(P)) ? (size_t)P.L * 24 : 0);
     if (lds > 65536) {  // once per instantiation (idempotent; not a stream operation)
         static bool raised = false;

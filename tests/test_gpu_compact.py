@@ -93,3 +93,29 @@ def test_compact_set_basis_and_oracle(spx, oracle):
         r = ctx.solve()
     assert r.status == spx.SolveStatus.OptimumFound
     assert abs(r.z - o.z) <= 1e-9 * abs(o.z)
+
+
+def test_compact_blocks_of_columns(spx, monkeypatch):
+    """m = 9000 (L > 8,192): the A_p gather runs in LDS blocks once S passes
+    8,192 columns; here a reinversion onto a basis of 8,500 structural
+    columns makes S = 8,500 at once.  Same pivots and close values as the
+    dense stream."""
+    m, n, seed = 9000, 18000, 4
+    with spx.Context(m=m, n=n, seed=seed, window=16, persist=False) as ctx:
+        basis = np.arange(n - m, n, dtype=np.int64)
+        basis[:8500] = np.arange(8500)  # structural columns 0..8499 in rows 0..8499
+        try:
+            ctx.set_basis(basis)
+        except spx.SimplexError:
+            pytest.skip("that basis is singular for this seed")
+        assert ctx.ftran_cols() == 8500
+        ctx.iterate(40)
+        a = ctx.state()
+    monkeypatch.setenv("SPX_DENSE_FTRAN", "1")
+    with spx.Context(m=m, n=n, seed=seed, window=16, persist=False) as ctx:
+        ctx.set_basis(basis)
+        assert ctx.ftran_cols() == m
+        ctx.iterate(40)
+        d = ctx.state()
+    assert np.array_equal(a["b_ixs"], d["b_ixs"])
+    assert _close(a["x_b"], d["x_b"], 1e-8)
