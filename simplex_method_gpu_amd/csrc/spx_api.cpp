@@ -446,7 +446,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
         x->lcfg.block = x->opts.loop_block;
-        HIP_TRY(loop_prepare(P, x->cus, x->lcfg));
+        HIP_TRY(loop_prepare(P, x->cus, x->lcfg, bc_possible(x, P)));
+        P.bc_lds = x->lcfg.bc_lds;
         // measured (tools/loop_sweep.sh): the persistent loop wins once the
         // base row is read from L2 (C5: 729 vs 681 it/s) and loses at C3
         // (8.3k vs 9.3k it/s), so by default only then
@@ -487,7 +488,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // compact FTRAN operand (Params::bc): two-kernel window passes on one
     // device-resident B_w with A[:, n-m:] = I (checked below, after the
     // upload), while A_p's gather fits beside the k_update LDS
-    x->bc_want = bc_possible(x, P) && !x->persist;
+    x->bc_want = bc_possible(x, P) && (!x->persist || x->lcfg.bc_lds > 0);
     if (x->opts.flags & SPX_FLAG_STAMPS) {
         SPX_TRY(x->alloc(&P.stamps, 32));
         SPX_TRY(reset_stamps(x));

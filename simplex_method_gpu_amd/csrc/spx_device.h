@@ -257,7 +257,7 @@ struct Params {
     // A[:, ns:] = I exactly (checked at create; SPX_DENSE_SLACKS=1 turns it
     // off): k_price prices a non-basic slack column without streaming it
     int32_t slack_unit;
-    int32_t pad_bc;
+    int32_t bc_lds;  // k_loop: doubles of A_p on the column list its LDS holds
     // B_w by its non-unit columns (eta window, two-kernel passes; DESIGN.md
     // §4a "compact FTRAN").  With A[:, ns:] = I, column k of B_w is e_k while
     // slack k has stayed basic in row k, so B_w = I + (columns rlist[0..S)).

@@ -52,13 +52,14 @@ struct LoopCfg {
     bool lds_r = true;  // pending base row in LDS next to y_w
     size_t lds_bytes = 0;
     bool ok = false;    // the persistent path is usable for this context
+    int bc_lds = 0;     // compact FTRAN operand: A_p-on-the-list doubles in LDS (0: none)
     int cpw = 0;        // tableau loop: list slots cached per wave
     int rw = 0;         // tableau loop: rows per wave
 };
 
 // Shapes the launch for P (window mode, one rank); ok = false when the device
 // cannot hold one workgroup per CU.
-hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c);
+hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c, bool want_bc = false);
 hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s);
 
 }  // namespace spx

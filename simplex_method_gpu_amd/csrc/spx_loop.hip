@@ -362,7 +362,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
 #ifndef SPX_LOOP_FPRE
 #define SPX_LOOP_FPRE 1
 #endif
-        const bool fpre = SPX_LOOP_FPRE && fr0 < row1 && FU * 64 <= L2;
+        const bool fpre = SPX_LOOP_FPRE && !P.bc && fr0 < row1 && FU * 64 <= L2;
         if (fpre) {
 #pragma unroll
             for (int t = 0; t < FU; ++t) {
@@ -425,12 +425,53 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
                 if (wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
             }
             const double s_x = upd_x ? sxw : 0.0;
+            // compact FTRAN operand (Params::bc, spx_kernels.hip k_update BC):
+            // A_p on the column list in LDS when it fits (else gathered per
+            // chunk), the same per-lane order, so the same bits as k_update
+            const int Sb = P.bc ? P.bc_n[0] : 0;
+            const bool apl = P.bc && Sb <= P.bc_lds;
+            double* apc = reinterpret_cast<double*>(smem + (LDS_R ? 2 : 1) * L * 8 + ((sizeof(Sh) + 15) / 16) * 16);
+            const double* apd = P.A + p * L;
+            if (apl) {
+                for (int c = tid; c < Sb; c += BLOCK) apc[c] = apd[P.rlist[c]];
+                __syncthreads();
+            }
+            auto compact_row = [&](int64_t i) -> double {
+                double a = (lane == 0 && P.rmap[i] < 0) ? apd[i] : 0.0;
+                const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + i * L2;
+                const int S2 = (Sb + 1) >> 1;
+                for (int k0 = 0; k0 < S2; k0 += 8 * 64) {
+                    dbl2 v[8], w[8];
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int k2 = k0 + lane + 64 * t;
+                        v[t] = brow[k2 < S2 ? k2 : 0];
+                        if (apl) {
+                            w[t] = reinterpret_cast<const dbl2*>(apc)[k2 < S2 ? k2 : 0];
+                        } else {
+                            const int c0 = 2 * (k2 < S2 ? k2 : 0);
+                            w[t].x = apd[P.rlist[c0]];
+                            w[t].y = c0 + 1 < Sb ? apd[P.rlist[c0 + 1]] : 0.0;
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int k2 = k0 + lane + 64 * t;
+                        if (2 * k2 < Sb) a = fma(v[t].x, w[t].x, a);
+                        if (2 * k2 + 1 < Sb) a = fma(v[t].y, w[t].y, a);
+                    }
+                }
+                return a;
+            };
             UpdPartial wp = upd_empty();
             for (int64_t i0 = row0 + wave; i0 < row1; i0 += 2 * WAVES) {
                 const int64_t i1 = i0 + WAVES;
                 const bool two = i1 < row1;
                 double acc[2] = {0.0, 0.0};
-                if (i0 == fr0)  // the prefetched pair (the first)
+                if (P.bc) {
+                    acc[0] = compact_row(i0);
+                    if (two) acc[1] = compact_row(i1);
+                } else if (i0 == fr0)  // the prefetched pair (the first)
                     ftran_rows2(ap, srcB + i0 * L2, two ? srcB + i1 * L2 : nullptr, L2, lane, pf0, pf1, fpre,
                                 acc[0], acc[1]);
                 else
@@ -553,6 +594,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
             st_agent(&P.nb_pos[leave], (int32_t)(cnt - 1));
             st_agent(&P.c_B[qn], c_p);
             st_agent(&P.b_ixs[qn], p);
+            if (P.rleft) st_agent(&P.rleft[qn], 1);  // (as pivot_bookkeeping: the compact operand's list)
             P.SY[nw] = s_y;
             st->aq = aqn;
             st->s_y = s_y;
@@ -613,7 +655,7 @@ static const void* fn_t() {
     return reinterpret_cast<const void*>(&k_loop<BLOCK, LR>);
 }
 
-hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c) {
+hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c, bool want_bc) {
     c.ok = false;
     c.block = 512;  // 8 waves per CU: 256 VGPRs per lane for the prefetch registers (1024 spilled)
     c.grid = cus;
@@ -623,6 +665,11 @@ hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c) {
     c.lds_r = 2 * ybytes + small <= cap;
     if (!c.lds_r && ybytes + small > cap) return hipSuccess;  // y_w alone does not fit
     c.lds_bytes = (c.lds_r ? 2 : 1) * ybytes + small;
+    if (want_bc) {  // compact FTRAN operand: A_p on the column list, what is left up to cap
+        const size_t room = cap - c.lds_bytes;
+        c.bc_lds = (int)std::min<size_t>((size_t)P.L, room / 8 / 64 * 64);
+        c.lds_bytes += (size_t)c.bc_lds * 8;
+    }
     int dev = 0, coop = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;

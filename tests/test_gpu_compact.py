@@ -119,3 +119,20 @@ def test_compact_blocks_of_columns(spx, monkeypatch):
         d = ctx.state()
     assert np.array_equal(a["b_ixs"], d["b_ixs"])
     assert _close(a["x_b"], d["x_b"], 1e-8)
+
+
+@pytest.mark.parametrize("window", [16, 64])
+def test_compact_persistent_loop_same_bits(spx, window):
+    """The persistent loop kernel (k_loop) runs the compact FTRAN with the
+    same per-lane order as k_update: the same alpha bits (so the same U and
+    B^-1) as two-kernel passes.  Its ratio-test partials group T = sum c_B
+    alpha by its own workgroups, so s_y and y agree to rounding (as with the
+    dense stream)."""
+    base = dict(m=600, n=2400, seed=3, window=window)
+    a = _run(spx, False, 300, persist=True, **base)
+    b = _run(spx, False, 300, persist=False, **base)
+    for key in ("b_ixs", "binv"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    for key in ("x_b", "y"):
+        assert _close(a[1][key], b[1][key], 1e-12), key
+    assert a[3].pivots == b[3].pivots and abs(a[3].z - b[3].z) <= 1e-12 * abs(b[3].z)

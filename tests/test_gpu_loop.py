@@ -91,12 +91,12 @@ def test_loop_refactor_and_timing(spx, oracle):
 
 def test_loop_auto_on_large_m(spx):
     """By default the persistent loop runs only where it measured faster: when
-    y_w and the pending base row do not both fit in LDS (m > ~9400).  It
-    streams the dense B_w; the two-kernel pass (persist=False) reads only
-    B_w's non-unit columns (the compact operand)."""
+    y_w and the pending base row do not both fit in LDS (m > ~9400).  Both
+    forms read only B_w's non-unit columns (the compact operand: none yet at
+    the slack basis)."""
     with spx.Context(m=1000, n=3000, seed=0, window=64) as ctx:
         assert ctx.config()["persistent"] == 0 and ctx.ftran_cols() == 0
     with spx.Context(m=12000, n=13000, seed=0, window=64) as ctx:
-        assert ctx.config()["persistent"] == 1 and ctx.ftran_cols() == 12000
+        assert ctx.config()["persistent"] == 1 and ctx.ftran_cols() == 0
     with spx.Context(m=12000, n=13000, seed=0, window=64, persist=False) as ctx:
         assert ctx.config()["persistent"] == 0 and ctx.ftran_cols() == 0
