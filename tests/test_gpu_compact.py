@@ -136,3 +136,20 @@ def test_compact_persistent_loop_same_bits(spx, window):
     for key in ("x_b", "y"):
         assert _close(a[1][key], b[1][key], 1e-12), key
     assert a[3].pivots == b[3].pivots and abs(a[3].z - b[3].z) <= 1e-12 * abs(b[3].z)
+
+
+@pytest.mark.parametrize("kw", [dict(m=257, n=1001, seed=6, window=16),
+                                dict(m=300, n=1200, seed=8, window=32, pricing=1),
+                                dict(m=300, n=1200, seed=8, window=16, ratio_test=2),
+                                dict(m=300, n=1200, seed=8, window=16, ratio_test=1)],
+                         ids=["odd-m", "devex", "harris", "guarded"])
+def test_compact_rules_and_odd_sizes(spx, kw):
+    """Odd m (a half-used last chunk), Devex pricing and the guarded / Harris
+    ratio tests: the compact operand takes the dense stream's pivots."""
+    a = _run(spx, False, 150, persist=False, **kw)
+    d = _run(spx, True, 150, persist=False, **kw)
+    assert np.array_equal(a[1]["b_ixs"], d[1]["b_ixs"])
+    assert np.array_equal(a[2], d[2])
+    assert _close(a[1]["x_b"], d[1]["x_b"], 1e-9)
+    assert a[3].status == d[3].status and a[3].pivots == d[3].pivots
+    assert abs(a[3].z - d[3].z) <= 1e-9 * max(1.0, abs(d[3].z))
