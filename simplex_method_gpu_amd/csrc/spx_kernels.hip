@@ -61,8 +61,14 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 // compact FTRAN (Params::bc): dbl2 chunks of each compact row requested at
 // k_update entry (256 columns), and column-list entries per thread requested
 // ahead of the entering column (1,024 columns at 512 threads)
-constexpr int BC_PF = 2;
-constexpr int BC_PF2 = 4;  // chunks requested once S is known (up to 512 columns)
+#ifndef SPX_BC_PF
+#define SPX_BC_PF 2
+#endif
+#ifndef SPX_BC_PF2
+#define SPX_BC_PF2 4
+#endif
+constexpr int BC_PF = SPX_BC_PF;
+constexpr int BC_PF2 = SPX_BC_PF2;  // chunks requested once S is known (up to 512 columns)
 constexpr int BC_APC = 8192;  // A_p gathered onto the list in LDS blocks of this many columns
 constexpr int BC_RL = 2;
 
