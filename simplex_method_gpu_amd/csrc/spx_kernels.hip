@@ -62,7 +62,7 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 // k_update entry (256 columns), and column-list entries per thread requested
 // ahead of the entering column (1,024 columns at 512 threads)
 #ifndef SPX_BC_PF
-#define SPX_BC_PF 2
+#define SPX_BC_PF 1  // C3 A/B (tools/r02_abbench.sh): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
 #endif
 #ifndef SPX_BC_PF2
 #define SPX_BC_PF2 4
