@@ -1020,6 +1020,10 @@ __device__ __forceinline__ void win_rows(const dbl2* __restrict__ a, const dbl2*
     }
 }
 
+// row i clamped into [0, m): an unconditional prefetch of a row past the end
+// reads the last row instead, and is never consumed
+__device__ __forceinline__ int64_t clamp_row(int64_t i, int64_t m) { return i < m ? i : m - 1; }
+
 template <int BLOCK, int R, bool RS, bool WIN, int BNT, bool BC>
 __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     DevState* st = P.st;
@@ -1056,13 +1060,14 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         // (compact FTRAN, P.bc: the first BC_PF chunks of this wave's
         // compact rows, the later ones re-requesting chunk 0 (cache hits), so
         // the loads stay unconditional and the waits below exact)
-        const int64_t prow = pf_row + R <= P.m ? pf_row : (P.m >= R ? P.m - R : 0);
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? P.bc : P.B0) + prow * L2c;
+        // (each row clamped on its own: in a partly filled last wave, row u <
+        // nvalid must be row pf_row + u, which the compact path consumes)
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? P.bc : P.B0);
 #pragma unroll
         for (int t = 0; t < PFU; ++t) {
             const int64_t k = (BC && t >= BC_PF) ? lane : (lane + t * 64 < L2c ? lane + t * 64 : L2c - 1);
 #pragma unroll
-            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[u * L2c + k]);
+            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[clamp_row(pf_row + u, P.m) * L2c + k]);
         }
     }
     // compact FTRAN: the column list and this wave's unit flags, ahead of p
@@ -1177,20 +1182,19 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if constexpr (BC) {
         Sbc = P.bc_n[0];
         const int64_t L2c = P.L >> 1;
-        const int64_t prow = pf_row + R <= P.m ? pf_row : (P.m >= R ? P.m - R : 0);
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.bc) + prow * L2c;
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.bc);
 #pragma unroll
         for (int t = BC_PF; t < BC_PF2; ++t) {
             const int k2 = lane + 64 * t;
             const int kk = (2 * k2 < Sbc && k2 < L2c) ? k2 : lane;
 #pragma unroll
-            for (int u = 0; u < R; ++u) pf2[t - BC_PF][u] = b0[u * L2c + kk];
+            for (int u = 0; u < R; ++u) pf2[t - BC_PF][u] = b0[clamp_row(pf_row + u, P.m) * L2c + kk];
         }
         const double* apd = P.A + p * P.L;
 #pragma unroll
         for (int j = 0; j < BC_RL; ++j) apv[j] = apd[rlv[j]];
 #pragma unroll
-        for (int u = 0; u < R; ++u) auv[u] = apd[prow + u];
+        for (int u = 0; u < R; ++u) auv[u] = apd[clamp_row(pf_row + u, P.m)];
     }
     const int64_t it = Sv.iter;
     const int par = (int)(it & 1);

@@ -1,0 +1,116 @@
+"""GPU parity at the two largest BASELINE configs, C4 (m=4096, n=131072) and
+C5 (m=16384, n=65536), against the oracle through two eta-window folds.
+
+The fixtures ``tests/golden/oracle_c{4,5}_k130.npz`` hold the oracle's
+(oracle/simplex_oracle.c, the restatement of v4_cub_reduction.cu:286-359)
+first 130 pivots from the slack basis, and its x_b, y and basis order after
+them (``tests/golden/make_golden_c45.py``, run in the build container: the
+oracle needs minutes and 11 GB of host memory at C5, too much for a GPU test).
+
+130 pivots = two 63-pivot windows, so every default path below runs its fold
+(k_fold, the compact-operand compaction k_bc_list / k_bc_gather) twice and
+its third window on the folded state:
+  - C4 default: two-kernel window passes with the compact FTRAN operand;
+  - C4 as an in-process group of 8 column shards (B^-1 replicated, MINLOC
+    merge; the north-star partitioning);
+  - C5 default: the persistent loop k_loop (compact FTRAN, A_p gathered on the
+    column list into LDS); C5 with two-kernel passes; C5 as a 2-shard group.
+Tolerances (fp64): (p, q) identical for every pivot; the same
+basis order; x_b and y within 1e-9 (relative max-norm); z within 1e-9.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REL = 1e-9
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _golden(name):
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"oracle_{name}_k130.npz"))
+    return {k: g[k] for k in g.files}
+
+
+def _check(spx, g, ctx):
+    K = int(g["k"])
+    tp, tq = ctx.trace()
+    s = ctx.state()
+    assert np.array_equal(tp, g["trace_p"]), int(np.argmax(tp != g["trace_p"]))
+    assert np.array_equal(tq, g["trace_q"]), int(np.argmax(tq != g["trace_q"]))
+    assert np.array_equal(s["b_ixs"], g["b_ixs"])
+    assert _rel(s["x_b"], g["x_b"]) <= REL
+    assert _rel(s["y"], g["y"]) <= REL
+    z = ctx.objective()
+    assert abs(z - float(g["z"])) <= REL * abs(float(g["z"]))
+    assert len(tp) == K
+
+
+def _single(spx, g, expect_persistent, **kw):
+    K = int(g["k"])
+    m, n, seed = int(g["m"]), int(g["n"]), int(g["seed"])
+    with spx.Context(m=m, n=n, seed=seed, eps=float(g["eps"]), trace=K, **kw) as ctx:
+        cfg = ctx.config()
+        assert cfg["window"] == 64, cfg  # the default representation at m >= 2048
+        assert bool(cfg["persistent"]) == expect_persistent, cfg
+        assert ctx.ftran_cols() < m  # the compact FTRAN operand
+        st, piv = ctx.iterate(K)
+        assert st == spx.SolveStatus.MaxIter and piv == K
+        _check(spx, g, ctx)
+
+
+def _group(spx, g, G, **kw):
+    K = int(g["k"])
+    m, n, seed = int(g["m"]), int(g["n"]), int(g["seed"])
+    ctxs = [spx.Context(m=m, n=n, seed=seed, eps=float(g["eps"]), rank=r, nranks=G, trace=K, **kw)
+            for r in range(G)]
+    try:
+        assert all(c.config()["window"] == 64 for c in ctxs)
+        st, piv = spx.group_iterate(ctxs, K)
+        assert st == spx.SolveStatus.MaxIter and piv == K
+        for c in ctxs:
+            _check(spx, g, c)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.fixture(scope="module")
+def c4():
+    g = _golden("c4")
+    assert (int(g["m"]), int(g["n"]), int(g["seed"])) == (4096, 131072, 0)
+    return g
+
+
+@pytest.fixture(scope="module")
+def c5():
+    g = _golden("c5")
+    assert (int(g["m"]), int(g["n"]), int(g["seed"])) == (16384, 65536, 0)
+    return g
+
+
+def test_c4_default_matches_oracle(spx, c4):
+    _single(spx, c4, expect_persistent=False)
+
+
+def test_c4_group8_matches_oracle(spx, c4):
+    _group(spx, c4, 8)
+
+
+def test_c5_default_persistent_matches_oracle(spx, c5):
+    _single(spx, c5, expect_persistent=True)
+
+
+def test_c5_two_kernel_matches_oracle(spx, c5):
+    _single(spx, c5, expect_persistent=False, persist=False)
+
+
+def test_c5_group2_matches_oracle(spx, c5):
+    _group(spx, c5, 2)

@@ -153,3 +153,25 @@ def test_compact_rules_and_odd_sizes(spx, kw):
     assert _close(a[1]["x_b"], d[1]["x_b"], 1e-9)
     assert a[3].status == d[3].status and a[3].pivots == d[3].pivots
     assert abs(a[3].z - d[3].z) <= 1e-9 * max(1.0, abs(d[3].z))
+
+
+@pytest.mark.parametrize("rows,m,n,window", [(2, 401, 1604, 16), (4, 257, 1028, 16), (8, 401, 1604, 64),
+                                             (4, 403, 1612, 8), (2, 301, 1204, 64)],
+                         ids=["r2-m401", "r4-m257", "r8-m401-w64", "r4-m403-w8", "r2-m301-w64"])
+def test_compact_partial_last_wave(spx, rows, m, n, window):
+    """m not a multiple of the rows per wave (nor of 16): the last wave of
+    k_update holds fewer than R rows, and its prefetched compact chunks and
+    unit terms must still belong to its own rows.  The
+    compact operand takes the dense stream's pivot path, with R rows per
+    wave and with one."""
+    kw = dict(m=m, n=n, seed=11, window=window, persist=False)
+    a = _run(spx, False, 200, update_rows=rows, **kw)
+    d = _run(spx, True, 200, update_rows=rows, **kw)
+    one = _run(spx, False, 200, **kw)
+    assert np.array_equal(a[2], d[2]) and np.array_equal(a[2], one[2])
+    assert np.array_equal(a[1]["b_ixs"], d[1]["b_ixs"])
+    for key in ("x_b", "binv"):
+        assert _close(a[1][key], d[1][key], 1e-10), key
+        assert np.array_equal(a[1][key], one[1][key]), key  # alpha has the per-lane order of R = 1
+    assert a[3].status == d[3].status and a[3].pivots == d[3].pivots
+    assert abs(a[3].z - d[3].z) <= 1e-9 * max(1.0, abs(d[3].z))
