@@ -353,12 +353,19 @@ def main():
                             "algorithmic_bytes_per_launch": fold_bytes,
                             "achieved_GBps": fold_bytes / (ks["fold_ms"] * 1e-3) / 1e9 if ks["fold_ms"] > 0 else 0.0}
                            if win else None),
-                "iteration": {"algorithmic_bytes_survey": b_alg,
-                              "achieved_GBps_survey": b_alg * value / 1e9,
-                              "frac_survey": b_alg * value / 1e9 / HBM_PEAK_GBS,
-                              "algorithmic_bytes_moved": b_moved,
-                              "achieved_GBps_moved": b_moved * value / 1e9,
-                              "frac_moved": b_moved * value / 1e9 / HBM_PEAK_GBS,
+                # whole-iteration roofline of this representation: the bytes
+                # it moves per pivot (pricing stream, FTRAN operand, fold / 63)
+                # over the pivot time.  SURVEY.md §8(d)'s B_alg counts the
+                # explicit representation's per-pivot B^-1 rewrite, which the
+                # window never does, so B_alg / time is only an equivalent
+                # rate, not a fraction of peak (the explicit block's
+                # iteration.frac is that representation's own roofline)
+                "iteration": {"algorithmic_bytes": b_moved,
+                              "achieved_GBps": b_moved * value / 1e9,
+                              "frac": b_moved * value / 1e9 / HBM_PEAK_GBS,
+                              "bytes_survey_B_alg": b_alg,
+                              "equivalent_GBps_survey": b_alg * value / 1e9,
+                              "explicit_iteration_frac": explicit["iteration"]["frac"] if explicit else None,
                               "event_timed_ms_per_step": 1e3 * ev_run["dt"] / max(ev_run["pivots"], 1),
                               "event_timed_dispatch": describe_dispatch(ev_run["dispatch"])},
             },

@@ -115,6 +115,19 @@ typedef struct spx_opts {
  *          spx_price's min_e is then the entering column's reduced cost. */
 #define SPX_PRICING_DANTZIG 0
 #define SPX_PRICING_DEVEX   1
+/* STEEPEST: steepest edge with a recurrence (README.md:16-17): exact weights
+ *          gamma_j = 1 + ||B^-1 A_j||^2, 1 + ||A_j||^2 at the slack basis,
+ *          kept by Goldfarb & Reid's update after a pivot with alpha = B^-1 A_p,
+ *          pivot element alpha_q, pivot row alpha_rj, g = alpha_rj / alpha_q,
+ *          gamma_p = 1 + ||alpha||^2 and d_j = A_j . B^-T alpha (B^-1 before
+ *          the pivot): gamma_j = max(gamma_j - 2 g d_j + g^2 gamma_p, 1 + g^2),
+ *          gamma_leave = max(gamma_p / alpha_q^2, 1); p = argmin of
+ *          -e_j^2/gamma_j over e_j < -eps.  d_j rides on the pricing pass's
+ *          A stream as a third dot (B_w^T alpha in LDS beside y_w and the base
+ *          row, plus the window terms), so it needs the window and one rank,
+ *          runs two-kernel passes, and not with the tableau.  spx_set_basis
+ *          restarts the weights at 1 + ||A_j||^2. */
+#define SPX_PRICING_STEEPEST 2
 
 /* Leaving-row rules.
  * REFERENCE: theta_i = x_b_i / alpha_i over alpha_i > 0, first index on ties
@@ -285,6 +298,11 @@ int spx_objective(spx_ctx* ctx, double* z);
  * (either may be NULL) and stores that count in *count.  Indexed by pivot
  * number, so a spx_reset / re-solve overwrites it. */
 int spx_get_trace(spx_ctx* ctx, int64_t* p, int64_t* q, int64_t cap, int64_t* count);
+
+/* Devex / steepest-edge pricing weights w_j of every column (n entries; the
+ * non-basic ones are the live weights, as updated by the last pricing pass).
+ * SPX_ERR_STATE under Dantzig pricing. */
+int spx_get_weights(spx_ctx* ctx, double* w);
 
 /* With SPX_FLAG_TIMING: total device milliseconds and launch counts of the
  * pricing kernel and of the fused update kernel since the last call (resets). */

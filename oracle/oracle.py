@@ -31,13 +31,13 @@ _lib = None
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
 # entering-column rules (include/simplex.h SPX_PRICING_*)
-PRICING_DANTZIG, PRICING_DEVEX = 0, 1
+PRICING_DANTZIG, PRICING_DEVEX, PRICING_STEEPEST = 0, 1, 2
 
 
 class OrcOpts(ctypes.Structure):
     _fields_ = [("max_iter", ctypes.c_int64), ("eps", ctypes.c_double), ("threads", ctypes.c_int),
                 ("ratio", ctypes.c_int), ("piv_tol", ctypes.c_double), ("feas_tol", ctypes.c_double),
-                ("refactor_every", ctypes.c_int64), ("pricing", ctypes.c_int)]
+                ("refactor_every", ctypes.c_int64), ("pricing", ctypes.c_int), ("w_out", ctypes.c_void_p)]
 
 
 def build() -> str:
@@ -169,6 +169,7 @@ class OracleResult:
     trace_q: np.ndarray
     y: np.ndarray | None = None
     binv: np.ndarray | None = None
+    weights: np.ndarray | None = None  # Devex / steepest-edge weights (want_state)
 
 
 def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 << 40,
@@ -192,13 +193,15 @@ def solve(A_cols: np.ndarray, b: np.ndarray, c: np.ndarray, max_iter: int = 1 <<
     o.max_iter, o.eps, o.threads = max_iter, eps, threads
     o.ratio, o.piv_tol, o.feas_tol, o.refactor_every = ratio, piv_tol, feas_tol, refactor_every
     o.pricing = pricing
+    w = np.zeros(n) if (want_state and pricing) else None
+    o.w_out = None if w is None else w.ctypes.data
     st = lib().orc_solve_ex(m, n, _ptr(A_cols), _ptr(b), _ptr(c), ctypes.byref(o),
                             ctypes.byref(z), _ptr(x_b), _ptr(b_ixs), ctypes.byref(piv),
                             _ptr(tp), _ptr(tq), trace_cap, _ptr(y), _ptr(binv))
     if st < 0:
         raise ValueError(f"orc_solve failed ({st})")
     k = min(piv.value, trace_cap)
-    return OracleResult(st, z.value, x_b, b_ixs, piv.value, tp[:k], tq[:k], y, binv)
+    return OracleResult(st, z.value, x_b, b_ixs, piv.value, tp[:k], tq[:k], y, binv, w)
 
 
 def reinvert(A_cols, b, c, basis, threads: int = 0):

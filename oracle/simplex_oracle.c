@@ -107,6 +107,10 @@ typedef struct {
     int dvx_pend;
     double dvx_aq, dvx_wp;
     int64_t dvx_leave;
+    /* steepest edge (orc_opts.pricing = 2): v = B^-T alpha of the last pivot
+     * (B^-1 before it) and gamma_p = 1 + ||alpha||^2, exact */
+    double* se_v;
+    double se_gp;
 } orc_state;
 
 static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
@@ -125,8 +129,9 @@ static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
     s->b_ixs = (int64_t*)malloc(sizeof(int64_t) * (size_t)m);
     s->w = (double*)malloc(sizeof(double) * (size_t)n);
     s->basic = (char*)calloc((size_t)n, 1);
+    s->se_v = (double*)malloc(sizeof(double) * (size_t)m);
     if (!s->Binv || !s->c_b || !s->x_b || !s->y || !s->e || !s->alpha ||
-        !s->theta || !s->E || !s->r || !s->b_ixs || !s->w || !s->basic)
+        !s->theta || !s->E || !s->r || !s->b_ixs || !s->w || !s->basic || !s->se_v)
         return -1;
     for (int64_t j = 0; j < n; ++j) s->w[j] = 1.0;
     for (int64_t j = n - m; j < n; ++j) s->basic[j] = 1;
@@ -146,7 +151,21 @@ static int state_init(orc_state* s, int64_t m, int64_t n, const double* b,
 static void state_free(orc_state* s) {
     free(s->Binv); free(s->c_b); free(s->x_b); free(s->y); free(s->e);
     free(s->alpha); free(s->theta); free(s->E); free(s->r); free(s->b_ixs);
-    free(s->w); free(s->basic);
+    free(s->w); free(s->basic); free(s->se_v);
+}
+
+/* Steepest-edge reference weights at the slack basis (B = I):
+ * gamma_j = 1 + ||A_j||^2, k ascending, for the structural columns (the slack
+ * columns are basic; their weights are set when they leave). */
+static void se_init(orc_state* s, const double* A) {
+    const int64_t m = s->m, n = s->n;
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < n - m; ++j) {
+        const double* col = A + j * m;
+        double a = 0.0;
+        for (int64_t k = 0; k < m; ++k) a = fma(col[k], col[k], a);
+        s->w[j] = 1.0 + a;
+    }
 }
 
 /* One pass of the do-loop body (v4:286-357).  Returns ORC_MAX_ITER when a
@@ -230,6 +249,59 @@ static int64_t devex_choose(orc_state* s, const double* A, double eps) {
     return p;
 }
 
+/* Steepest-edge entering column (README.md:16-17 "Steepest edge with a
+ * recurrence"): exact reference weights gamma_j = 1 + ||B^-1 A_j||^2, kept by
+ * Goldfarb & Reid's recurrence.  After a pivot with entering p, leaving row q,
+ * alpha = B^-1 A_p, alpha_q = alpha[q], pivot row alpha_rj = r.A_j (r = row q
+ * of B^-1 before the pivot), v = B^-T alpha and gamma_p = 1 + ||alpha||^2
+ * (both before the pivot), every non-basic column j but the leaving one takes
+ *   g = alpha_rj / alpha_q,  d_j = v.A_j,
+ *   gamma_j = max(gamma_j - 2 g d_j + g^2 gamma_p, 1 + g^2)
+ *           = fmax(fma(g*g, gamma_p, fma(-2*g, d_j, gamma_j)), fma(g, g, 1)),
+ * and the leaving column gamma = max(gamma_p / alpha_q^2, 1).  Then p =
+ * argmin over non-basic j with e_j < -eps of -(e_j^2) / gamma_j (first index
+ * on ties); -1 when there is none (optimal).  Weights start at the slack basis
+ * (se_init) and persist across reinversions. */
+static void se_apply_pending(orc_state* s, const double* A) {
+    const int64_t m = s->m, n = s->n;
+    if (s->dvx_pend) {
+        const double aq = s->dvx_aq, gp = s->se_gp;
+#pragma omp parallel for schedule(static)
+        for (int64_t j = 0; j < n; ++j) {
+            if (s->basic[j]) continue;
+            if (j == s->dvx_leave) {
+                const double v = gp / (aq * aq);
+                s->w[j] = v > 1.0 ? v : 1.0;
+                continue;
+            }
+            const double* col = A + j * m;
+            double a = 0.0, d = 0.0;
+            for (int64_t k = 0; k < m; ++k) {
+                a = fma(s->r[k], col[k], a);
+                d = fma(s->se_v[k], col[k], d);
+            }
+            const double g = a / aq;
+            const double t = fma(g * g, gp, fma(-2.0 * g, d, s->w[j]));
+            const double lo = fma(g, g, 1.0);
+            s->w[j] = t > lo ? t : lo;
+        }
+        s->dvx_pend = 0;
+    }
+}
+
+static int64_t se_choose(orc_state* s, const double* A, double eps) {
+    const int64_t n = s->n;
+    se_apply_pending(s, A);
+    int64_t p = -1;
+    double best = INFINITY;
+    for (int64_t j = 0; j < n; ++j) {
+        if (s->basic[j] || !(s->e[j] < -eps)) continue;
+        const double key = -(s->e[j] * s->e[j]) / s->w[j];
+        if (key < best) { best = key; p = j; }
+    }
+    return p;
+}
+
 static int one_pass(orc_state* s, const double* A, const double* b,
                     const double* c, double eps, int rule, double piv_tol,
                     double feas_tol, int pricing, int64_t* p_out, int64_t* q_out) {
@@ -239,8 +311,8 @@ static int one_pass(orc_state* s, const double* A, const double* b,
     /* pricing GEMM + entering ArgMin (v4:289-302), or Devex */
     orc_price(m, n, A, c, s->y, s->e, 0);
     int64_t p;
-    if (pricing == 1) {
-        p = devex_choose(s, A, eps);
+    if (pricing == 1 || pricing == 2) {
+        p = pricing == 1 ? devex_choose(s, A, eps) : se_choose(s, A, eps);
         if (p < 0) return ORC_OPTIMUM_FOUND;
     } else {
         p = argmin_first(s->e, n, &min_val);
@@ -266,6 +338,21 @@ static int one_pass(orc_state* s, const double* A, const double* b,
     /* compute_theta + leaving ArgMin (v4:199-208,317-325), or a variant */
     const int64_t q = ratio_test(s, rule, piv_tol, feas_tol);
     if (q < 0) return ORC_UNBOUNDED;
+
+    /* steepest edge: v = B^-T alpha and gamma_p = 1 + ||alpha||^2 with the
+     * B^-1 of before this pivot (se_choose applies them at the next pass) */
+    if (pricing == 2) {
+        double a2 = 0.0;
+        for (int64_t i = 0; i < m; ++i) a2 = fma(s->alpha[i], s->alpha[i], a2);
+        s->se_gp = 1.0 + a2;
+#pragma omp parallel for schedule(static)
+        for (int64_t k = 0; k < m; ++k) {
+            const double* colk = s->Binv + k * m;
+            double v = 0.0;
+            for (int64_t i = 0; i < m; ++i) v = fma(colk[i], s->alpha[i], v);
+            s->se_v[k] = v;
+        }
+    }
 
     /* r = B_inv[q,:] (cublasScopy, v4:331); E_q (compute_E_q v4:210-215) */
     for (int64_t k = 0; k < m; ++k) s->r[k] = s->Binv[q + k * m];
@@ -423,6 +510,7 @@ void orc_default_opts(orc_opts* o) {
     o->feas_tol = 1e-9;
     o->refactor_every = 0;
     o->pricing = 0;
+    o->w_out = NULL;
 }
 
 int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
@@ -434,6 +522,7 @@ int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
     set_threads(o->threads);
     orc_state s;
     if (state_init(&s, m, n, b, c) != 0) { state_free(&s); return -2; }
+    if (o->pricing == 2) se_init(&s, A);
 
     int status = ORC_MAX_ITER;
     int64_t i = 0;
@@ -466,6 +555,10 @@ int orc_solve_ex(int64_t m, int64_t n, const double* A, const double* b,
     if (binv_out)
         for (int64_t r = 0; r < m; ++r)
             for (int64_t k = 0; k < m; ++k) binv_out[r * m + k] = s.Binv[r + k * m];
+    if (o->w_out) {  /* the current weights: the last pivot's update applied */
+        if (o->pricing == 2) se_apply_pending(&s, A);
+        memcpy(o->w_out, s.w, sizeof(double) * (size_t)n);
+    }
     state_free(&s);
     return status;
 }

@@ -74,7 +74,9 @@ typedef struct {
     double piv_tol;
     double feas_tol;
     int64_t refactor_every;
-    int pricing; /* 0 Dantzig (v4:288-302), 1 Devex (simplex_oracle.c devex_choose) */
+    int pricing; /* 0 Dantzig (v4:288-302), 1 Devex (simplex_oracle.c devex_choose),
+                    2 steepest edge with the Goldfarb-Reid recurrence (se_choose) */
+    double* w_out; /* optional: the final pricing weights (n), Devex / steepest edge */
 } orc_opts;
 
 void orc_default_opts(orc_opts* o);

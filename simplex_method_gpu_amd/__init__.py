@@ -25,7 +25,7 @@ from ._lib import SimplexError, SpxOpts, check, load
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
            "shard_range", "minloc_merge", "group_iterate", "group_sync",
            "SimplexError", "FLAG_TIMING", "RATIO_REFERENCE", "RATIO_GUARDED", "RATIO_HARRIS",
-           "PRICING_DANTZIG", "PRICING_DEVEX"]
+           "PRICING_DANTZIG", "PRICING_DEVEX", "PRICING_STEEPEST"]
 
 FLAG_TIMING = 1
 FLAG_STAMPS = 2
@@ -43,7 +43,7 @@ FLAG_PRICE_TAIL = 1024  # k_price's last workgroup merges the entering candidate
 # leaving-row rules (include/simplex.h SPX_RATIO_*)
 RATIO_REFERENCE, RATIO_GUARDED, RATIO_HARRIS = 0, 1, 2
 # entering-column rules (include/simplex.h SPX_PRICING_*)
-PRICING_DANTZIG, PRICING_DEVEX = 0, 1
+PRICING_DANTZIG, PRICING_DEVEX, PRICING_STEEPEST = 0, 1, 2
 
 
 class SolveStatus(IntEnum):
@@ -145,7 +145,7 @@ class Context:
         o.window = window  # 0 auto, -1 explicit rank-1 B^-1 update, 8/16/32/64 eta window
         o.ratio_test, o.piv_tol, o.feas_tol = ratio_test, piv_tol, feas_tol  # RATIO_*
         o.refactor_every = refactor_every
-        o.pricing = pricing  # PRICING_DANTZIG / PRICING_DEVEX
+        o.pricing = pricing  # PRICING_DANTZIG / PRICING_DEVEX / PRICING_STEEPEST
         o.loop_block = loop_block
         o.trace_cap = trace  # record the first `trace` pivots' (p, q) on the device
         o.flags = ((FLAG_TIMING if timing else 0) | (FLAG_STAMPS if stamps else 0)
@@ -236,6 +236,12 @@ class Context:
         check(self._L.spx_solve(self._h, max_iter, ctypes.byref(z), _ptr(b_ixs), _ptr(x_b),
                                 ctypes.byref(st), ctypes.byref(piv)))
         return SolveResult(z.value, SolveStatus(st.value), x_b, b_ixs, piv.value)
+
+    def weights(self):
+        """Devex / steepest-edge pricing weights of every column (spx_get_weights)."""
+        w = np.empty(self.n, dtype=np.float64)
+        check(self._L.spx_get_weights(self._h, _ptr(w)))
+        return w
 
     def trace(self):
         """(entering columns, leaving rows) of the pivots recorded so far

@@ -23,7 +23,7 @@
 //   --piv-tol T, --feas-tol T   tolerances of the guarded / Harris rules
 //   --refactor K   rebuild B^-1 from the basis every K pivots (spx_reinvert)
 //   --window W     B^-1 representation (0 auto, -1 explicit, 8..64 eta window)
-//   --pricing P    entering-column rule: dantzig (v4:288-302, default) | devex
+//   --pricing P    entering-column rule: dantzig (v4:288-302, default) | devex | steepest
 //   --tableau      window tableau (SPX_FLAG_TABLEAU): T_w = B_w A
 //                  kept in HBM, no per-pivot A / B^-1 stream
 //   --mps          the input is an MPS file (mps_io.h): converted to the
@@ -68,7 +68,7 @@ static void print_elapsed_time(const char* msg, double dur) {
 static void usage() {
     std::cerr << "usage: solver [--max-iter K] [--eps E] [--compat] [--device D] [--no-iter-lines] [--json]"
                  " [--threads T] [--write-bin F] [--write-text F] [--no-solve] [--ratio reference|guarded|harris]"
-                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--pricing dantzig|devex] [--tableau]"
+                 " [--piv-tol T] [--feas-tol T] [--refactor K] [--window W] [--pricing dantzig|devex|steepest] [--tableau]"
                  " [--mps [--big-m M]]"
                  " (<file> | --gen m n seed)\n";
 }
@@ -124,7 +124,10 @@ int main(int argc, char* argv[]) {
         else if (s == "--pricing") {
             need(1);
             const std::string r = argv[++a];
-            pricing = r == "dantzig" ? SPX_PRICING_DANTZIG : r == "devex" ? SPX_PRICING_DEVEX : -1;
+            pricing = r == "dantzig" ? SPX_PRICING_DANTZIG
+                      : r == "devex"   ? SPX_PRICING_DEVEX
+                      : r == "steepest" ? SPX_PRICING_STEEPEST
+                                        : -1;
             if (pricing < 0) { usage(); return 1; }
         }
         else if (s == "--big-m") { need(1); big_m = std::strtod(argv[++a], nullptr); }

@@ -217,6 +217,7 @@ namespace {
 int reset_stamps(spx_ctx* x);
 
 bool env_on(const char* name);
+bool env_off(const char* name);
 // the compact FTRAN operand applies: eta window (no tableau, replicated
 // storage) and A[:, n-m:] = I (x->slack_ident, known before setup)
 bool bc_possible(const spx_ctx* x, const Params& P) {
@@ -328,12 +329,17 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         KW = (pays && !P.row_shard) ? 64 : -1;
     }
     // Devex pricing takes the pivot row from the eta-window pricing pass
-    if (x->opts.pricing != SPX_PRICING_DANTZIG && x->opts.pricing != SPX_PRICING_DEVEX)
+    if (x->opts.pricing != SPX_PRICING_DANTZIG && x->opts.pricing != SPX_PRICING_DEVEX &&
+        x->opts.pricing != SPX_PRICING_STEEPEST)
         return fail(SPX_ERR_ARG, "bad pricing %d", x->opts.pricing);
-    P.devex = x->opts.pricing == SPX_PRICING_DEVEX ? 1 : 0;
+    // steepest edge rides on Devex's plumbing (key -e^2/w, reduced-cost hand-off)
+    P.steep = x->opts.pricing == SPX_PRICING_STEEPEST ? 1 : 0;
+    P.devex = (x->opts.pricing == SPX_PRICING_DEVEX || P.steep) ? 1 : 0;
     if (P.devex) {
-        if (G > 1) return fail(SPX_ERR_ARG, "Devex pricing runs on one rank");
-        if (x->opts.window < 0) return fail(SPX_ERR_ARG, "Devex pricing needs the eta window (window > 0 or 0 = auto)");
+        const char* rule = P.steep ? "steepest-edge" : "Devex";
+        if (G > 1) return fail(SPX_ERR_ARG, "%s pricing runs on one rank", rule);
+        if (x->opts.window < 0) return fail(SPX_ERR_ARG, "%s pricing needs the eta window (window > 0 or 0 = auto)", rule);
+        if (P.steep && (x->opts.flags & SPX_FLAG_TABLEAU)) return fail(SPX_ERR_ARG, "steepest-edge pricing runs without the tableau");
         if (x->opts.window == 0) KW = 64;
         SPX_TRY(x->alloc(&P.W, (size_t)n));
         SPX_TRY(x->alloc(&P.dvx_e, 1));
@@ -351,6 +357,12 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         return fail(SPX_ERR_ARG, "window must be 8, 16, 32 or 64 (got %d)", KW);
     if (KW < -1) return fail(SPX_ERR_ARG, "bad window %d", KW);
     P.win = KW > 0 ? KW : 0;
+    if (P.steep) {  // B_w^T alpha (L), U^T alpha + gamma_p (KW + 1), row-block partials
+        P.se_parts = se_parts_for(m);
+        SPX_TRY(x->alloc(&P.se_v, (size_t)L));
+        SPX_TRY(x->alloc(&P.se_cg, (size_t)(KW + 1)));
+        SPX_TRY(x->alloc(&P.se_part, (size_t)P.se_parts * (size_t)(L + KW + 1)));
+    }
     if (P.win) {
         SPX_TRY(x->alloc(&P.U, (size_t)(m * KW)));
         SPX_TRY(x->alloc(&P.Wt, (size_t)((n + 1) * KW)));
@@ -389,7 +401,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // eta window: the pending base row next to y when both fit; the tableau
     // pass stages nothing (wm 3)
     pc.wm = P.tab ? 3 : (!P.win ? 0 : ((pc.lds_y && 2 * ybytes + red_bytes <= lds_cap) ? 1 : 2));
-    pc.lds_bytes = (pc.lds_y ? ybytes : 0) + (pc.wm == 1 ? ybytes : 0) + red_bytes;
+    // steepest edge: B_w^T alpha beside y and the base row when all three fit
+    if (P.steep) pc.wm = (pc.lds_y && 3 * ybytes + red_bytes <= lds_cap) ? 4 : 5;
+    pc.lds_bytes = (pc.lds_y ? ybytes : 0) + ((pc.wm == 1 || pc.wm == 4) ? ybytes : 0) + (pc.wm == 4 ? ybytes : 0) +
+                   red_bytes;
     int per_cu = 0;
     HIP_TRY(price_prepare(pc, &per_cu));
     if (per_cu < 1) per_cu = 1;
@@ -426,6 +441,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
     uc.block = ub;
     uc.rows = rows;
+    uc.bc_entry = !env_off("SPX_FTRAN_BC_ENTRY");
     const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
     uc.grid = (int)std::max<int64_t>(1, (P.mloc + rows_per_wg - 1) / rows_per_wg);
     if (P.tab) {  // k_tab_update: one lane per row, 256 rows per workgroup
@@ -443,7 +459,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (!P.tab && !(x->opts.flags & SPX_FLAG_COUNTED_TAIL))
         SPX_TRY(x->alloc(&P.price_tag, (size_t)(PRICE_WORDS * pc.grid)));
     // the persistent loop kernel replaces the two-kernel pass where it applies
-    if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !(x->opts.flags & SPX_FLAG_STAMPS) &&
+    if (P.win && !P.tab && G == 1 && !P.row_shard && P.ratio != RATIO_HARRIS && !P.steep &&
+        !(x->opts.flags & SPX_FLAG_STAMPS) &&
         !(x->opts.flags & (SPX_FLAG_NO_PERSIST | SPX_FLAG_COMM1))) {
         x->lcfg.block = x->opts.loop_block;
         HIP_TRY(loop_prepare(P, x->cus, x->lcfg, bc_possible(x, P)));
@@ -547,6 +564,7 @@ int do_reset(spx_ctx* x) {
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
     HIP_TRY(launch_reset(x->P, x->stream));
+    HIP_TRY(launch_se_init(x->P, x->stream));  // steepest edge: gamma_j = 1 + ||A_j||^2
     if (x->P.bc) {  // B_w = I: no column list
         HIP_TRY(hipMemsetAsync(x->P.rleft, 0, (size_t)x->L * sizeof(int32_t), x->stream));
         HIP_TRY(hipMemsetAsync(x->P.rmap, 0xFF, (size_t)x->L * sizeof(int32_t), x->stream));
@@ -629,6 +647,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
     }
     advance_window(x, fold);
+    HIP_TRY(launch_se_prep(x->P, x->stream));  // steepest edge: after the fold, before pricing
     Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
     Pp.defer_price = x->defer_ok ? 1 : 0;
     HIP_TRY(launch_price(Pp, x->pcfg, x->stream, p0, p1));
@@ -970,6 +989,10 @@ bool env_on(const char* name) {
     const char* env = std::getenv(name);
     return env && env[0] == '1';
 }
+bool env_off(const char* name) {
+    const char* env = std::getenv(name);
+    return env && env[0] == '0';
+}
 bool slack_identity(const double* A, int64_t m, int64_t n) {
     if (!A) return true;
     for (int64_t i = 0; i < m; ++i) {
@@ -1204,10 +1227,13 @@ int spx_set_basis(spx_ctx* x, const int64_t* basis) {
     st.leave = -1;  // Devex: a fresh reference framework
     st.wp = 1.0;
     HIP_TRY(hipMemcpy(x->P.st, &st, sizeof(st), hipMemcpyHostToDevice));
-    if (x->P.W) {
+    if (x->P.W && !x->P.steep) {
         const std::vector<double> ones((size_t)x->n, 1.0);
         HIP_TRY(hipMemcpy(x->P.W, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice));
     }
+    // steepest edge: the slack-basis reference values 1 + ||A_j||^2 (exact
+    // weights for an arbitrary basis would need B^-1 A in full)
+    HIP_TRY(launch_se_init(x->P, x->stream));
     x->broken = true;  // until the inverse is rebuilt
     SPX_TRY(reinvert_basis(x, basis));
     x->broken = false;
@@ -1361,6 +1387,14 @@ int spx_get_trace(spx_ctx* x, int64_t* p, int64_t* q, int64_t cap, int64_t* coun
     return SPX_OK;
 }
 
+int spx_get_weights(spx_ctx* x, double* w) {
+    if (!x || !w) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->P.W) return fail(SPX_ERR_STATE, "no pricing weights: the context runs Dantzig pricing");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    HIP_TRY(hipMemcpy(w, x->P.W, sizeof(double) * (size_t)x->n, hipMemcpyDeviceToHost));
+    return SPX_OK;
+}
+
 int spx_get_state(spx_ctx* x, double* x_b, int64_t* b_ixs, double* y, double* c_b, double* binv, int32_t* status,
                   int64_t* pivots) {
     if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
@@ -1436,6 +1470,7 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
     ++x->n_eager;
     x->n_folds += fold ? 1 : 0;
+    HIP_TRY(launch_se_prep(x->P, x->stream));
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
     const int ps = x->P.pr_stride;
     if (x->use_comm) {

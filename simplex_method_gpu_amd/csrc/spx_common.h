@@ -56,6 +56,17 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 // two butterflies interleaved (their cross-lane latencies overlap)
+__device__ __forceinline__ void wave_sum3(double& a, double& b, double& c) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ta = __shfl_xor(a, off, 64);
+        const double tb = __shfl_xor(b, off, 64);
+        const double tc = __shfl_xor(c, off, 64);
+        a += ta;
+        b += tb;
+        c += tc;
+    }
+}
 __device__ __forceinline__ void wave_sum2(double& a, double& b) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

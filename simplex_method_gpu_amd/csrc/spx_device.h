@@ -214,8 +214,20 @@ struct Params {
     int32_t devex;         // SPX_PRICING_DEVEX (eta window, one rank)
     double piv_tol;
     double feas_tol;
-    double* W;             // Devex reference weights (n)
+    double* W;             // Devex / steepest-edge reference weights (n)
     double* dvx_e;         // Devex: reduced cost of the chosen column (k_price -> k_update)
+    // steepest edge (SPX_PRICING_STEEPEST: devex = 1 as well, so the key,
+    // optimality test and reduced-cost plumbing are Devex's): exact weights
+    // gamma_j = 1 + ||B^-1 A_j||^2 kept by the Goldfarb-Reid recurrence.  For
+    // the pending pivot (alpha = its FTRAN column, B^-1 before it):
+    // se_v = B_w^T alpha (L), se_cg[s] = U[:, s] . alpha for s < tau and
+    // se_cg[KW] = gamma_p = 1 + ||alpha||^2 (k_se_part / k_se_fin before each
+    // pricing pass), so that A_j . B^-T alpha = se_v . A_j + sum_s se_cg[s] Wt[j][s]
+    int32_t steep;
+    int32_t se_parts;      // k_se_part workgroups (row blocks)
+    double* se_v;
+    double* se_cg;
+    double* se_part;       // se_parts x se_ncols partial sums
     // deferred pricing tail (one rank, captured/eager passes): k_price stores
     // its workgroup partials and returns; every k_update workgroup reduces the
     // price_grid partials itself (no last-workgroup fan-in, no ticket)

@@ -9,7 +9,8 @@ namespace spx {
 struct PriceCfg {
     int block;         // 256 / 512 / 1024 threads
     bool lds_y;        // stage y in LDS (L*8 bytes) or read it from global
-    int wm;            // 0 explicit B^-1; eta window: 1 base row in LDS, 2 in global
+    int wm;            // 0 explicit B^-1; eta window: 1 base row in LDS, 2 in global; 3 tableau;
+                       // 4 / 5 = 1 / 2 with steepest edge (B_w^T alpha in LDS / global)
     size_t lds_bytes;  // dynamic LDS per workgroup
     int grid;          // workgroups (persistent-style, grid-stride over columns)
 };
@@ -18,6 +19,7 @@ struct UpdateCfg {
     int block;  // threads per workgroup (256 / 512 / 1024)
     int rows;   // B^-1 rows per wave (1/2/4/8)
     int grid;   // ceil(m / (block / 64 * rows))
+    int bc_entry;  // compact FTRAN, 1 row per wave: k_ftran_bc (1) or k_update<..., BC> (0)
 };
 
 bool kernels_inplace();  // B^-1 updated in place (one buffer) or ping-pong
@@ -36,5 +38,10 @@ hipError_t launch_materialize(const Params& P, double* out, hipStream_t s);
 hipError_t launch_reduced_costs(const Params& P, double* e, hipStream_t s);
 hipError_t launch_objective(const Params& P, hipStream_t s);
 hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s);
+// steepest edge (P.steep): weights at the slack basis; B_w^T alpha, U^T alpha
+// and gamma_p of the pending pivot before a pricing pass
+hipError_t launch_se_init(const Params& P, hipStream_t s);
+hipError_t launch_se_prep(const Params& P, hipStream_t s);
+int se_parts_for(int64_t m);
 
 }  // namespace spx

@@ -127,13 +127,17 @@ __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, 
 // WM: 0 = explicit B^-1 (y updated in the LDS fill); 1 = eta window with the
 // pending base row in LDS next to y; 2 = eta window, base row read from global
 // (L2) when y and the row do not both fit; 3 = window tableau (P.tab): no A
-// stream, each column reads T_w[q_tau, j], dw[j] and its Wt row.
+// stream, each column reads T_w[q_tau, j], dw[j] and its Wt row; 4 / 5 = 1 / 2
+// with steepest-edge pricing (P.steep): a third dot v.A_j per column, v =
+// B_w^T alpha (P.se_v) in LDS beside y and the base row (4) or from global (5).
 template <int BLOCK, bool LDS_Y, int WM>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
     constexpr int WAVES = BLOCK / 64;
     constexpr bool WIN = WM != 0;
-    constexpr bool LDS_R = WM == 1;
+    constexpr bool LDS_R = WM == 1 || WM == 4;
+    constexpr bool SE = WM == 4 || WM == 5;
+    constexpr bool LDS_V = WM == 4;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -150,8 +154,9 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int64_t L2 = L >> 1;
     double* ys = reinterpret_cast<double*>(smem);
     double* rs = reinterpret_cast<double*>(smem + (LDS_Y ? L * 8 : 0));
-    PricePartial* red =
-        reinterpret_cast<PricePartial*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0));
+    double* vs = reinterpret_cast<double*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0));
+    PricePartial* red = reinterpret_cast<PricePartial*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0) +
+                                                        (LDS_V ? L * 8 : 0));
     int* s_last = reinterpret_cast<int*>(red + WAVES);
     const int nb = S.nb_count;
 
@@ -184,6 +189,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
               : (P.row_shard ? P.rbuf : ((SPX_INPLACE || WIN || !(it & 1)) ? P.B0 : P.B1) + qq * L));
     const bool stage_r = WIN ? (pend && wg0) : (SPX_INPLACE && pend && wg0 && !P.row_shard);
     const bool stage = LDS_Y || LDS_R || wg0;
+    const dbl2* vin = reinterpret_cast<const dbl2*>(P.se_v);  // steepest edge: B_w^T alpha
     const bool load_y = LDS_Y || (!WIN && wg0);
     const bool need_r = WIN ? (pend && (LDS_R || stage_r)) : (upd_y || stage_r);
 
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // so the fill waits for its own loads only, not for the A prefetch.
     constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
     const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
-    dbl2 yv[YB], rv[YB];
+    dbl2 yv[YB], rv[YB], vv[YB];
     double uqrow = 0.0;  // U[q][tid] for Urows (window, workgroup 0)
     if (stage) {
 #pragma unroll
@@ -203,6 +209,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             const int64_t kc = k < L2 ? k : L2 - 1;
             if (load_y) yv[u] = yin[kc];
             rv[u] = rr[kc];
+            if constexpr (LDS_V) vv[u] = vin[kc];
         }
         if constexpr (WIN) uqrow = P.U[qq * KW + (tid < KW ? tid : KW - 1)];
     }
@@ -224,10 +231,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         for (int u = 0; u < YB; ++u) {
             if (load_y) asm volatile("" ::"v"(yv[u].x), "v"(yv[u].y));
             asm volatile("" ::"v"(rv[u].x), "v"(rv[u].y));
+            if constexpr (LDS_V) asm volatile("" ::"v"(vv[u].x), "v"(vv[u].y));
         }
         if constexpr (WIN) asm volatile("" ::"v"(uqrow));
         dbl2* yl = reinterpret_cast<dbl2*>(ys);
         dbl2* rl = reinterpret_cast<dbl2*>(rs);
+        dbl2* vl = reinterpret_cast<dbl2*>(vs);
         dbl2* rb = reinterpret_cast<dbl2*>(WIN ? P.Qrows + (int64_t)tau * L : P.rbuf);
         for (int64_t k0 = 0; k0 < L2; k0 += (int64_t)YB * BLOCK) {
             if (k0 > 0) {  // later batches (L2 > YB * BLOCK)
@@ -237,6 +246,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     const int64_t kc = k < L2 ? k : L2 - 1;
                     if (load_y) yv[u] = yin[kc];
                     if (need_r) rv[u] = rr[kc];
+                    if constexpr (LDS_V) vv[u] = vin[kc];
                 }
             }
 #pragma unroll
@@ -251,6 +261,9 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                         if constexpr (LDS_Y) yl[k] = yv[u];
                         if constexpr (LDS_R) {
                             if (pend) rl[k] = rv[u];
+                        }
+                        if constexpr (LDS_V) {
+                            if (pend) vl[k] = vv[u];
                         }
                     }
                     if (stage_r) rb[k] = rv[u];
@@ -271,15 +284,22 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if constexpr (LDS_R) return reinterpret_cast<const dbl2*>(rs)[k];
         else return rr[k];
     };
+    auto Vw = [&](int64_t k) -> dbl2 {
+        if constexpr (LDS_V) return reinterpret_cast<const dbl2*>(vs)[k];
+        else return vin[k];
+    };
     // window coefficients of this lane (lane s < tau: pivot s of the window)
     double uq = 0.0, syl = 0.0, syp = 0.0;
+    double csl = 0.0, se_gp = 0.0;  // steepest edge: U[:, s] . alpha (lane s), gamma_p
     if constexpr (WIN) {
         if (pend) {
             if (lane < tau) {
                 uq = P.U[qq * KW + lane];
                 syl = P.SY[lane];
+                if constexpr (SE) csl = P.se_cg[lane];
             }
             syp = P.SY[tau];
+            if constexpr (SE) se_gp = P.se_cg[KW];
         }
     }
     double best = INFINITY, bw = 0.0, be = 0.0;
@@ -291,17 +311,28 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int nlist = nb;
     const int stride = gridDim.x * WAVES;
     // candidate update shared by every mode: Devex key, then the argmin
-    auto consider = [&](int64_t j, double e, double wn) {
+    auto consider = [&](int64_t j, double e, double wn, double dd) {
         double key = e;
         if (WIN && P.devex) {
             // Devex (include/simplex.h SPX_PRICING_DEVEX): the pending pivot's
-            // row entry wn = r.A_j updates this column's reference weight
+            // row entry wn = r.A_j updates this column's reference weight.
+            // Steepest edge (SPX_PRICING_STEEPEST, oracle se_choose): the
+            // Goldfarb-Reid recurrence with dd = A_j . B^-T alpha
             double w = P.W[j];
             if (pend) {
-                if (j == dvx_leave) w = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
-                else {
-                    const double g = wn / dvx_aq;
-                    w = fmax(w, g * g * dvx_wp);
+                if constexpr (SE) {
+                    if (j == dvx_leave) w = fmax(se_gp / (dvx_aq * dvx_aq), 1.0);
+                    else {
+                        const double g = wn / dvx_aq;
+                        const double t = fma(g * g, se_gp, fma(-2.0 * g, dd, w));
+                        w = fmax(t, fma(g, g, 1.0));
+                    }
+                } else {
+                    if (j == dvx_leave) w = fmax(dvx_wp / (dvx_aq * dvx_aq), 1.0);
+                    else {
+                        const double g = wn / dvx_aq;
+                        w = fmax(w, g * g * dvx_wp);
+                    }
                 }
                 if (lane == 0) P.W[j] = w;
             }
@@ -359,7 +390,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
         double wv = 0.0;
         if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
-        double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+        double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0, d0 = 0.0, d1 = 0.0;
         int64_t k = lane;
         const bool unit = unit_col(j);
         // Two 8-chunk batches in flight through the column: the batch after
@@ -373,11 +404,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 #pragma unroll
                 for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
                     if (h >= nb8) break;
-                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH];
+                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH], x[SPX_LDS_BATCH];
 #pragma unroll
                     for (int u = 0; u < SPX_LDS_BATCH; ++u) {
                         w[u] = Y(kb + lane + (h + u) * 64);
                         if constexpr (PD) r[u] = Rw(kb + lane + (h + u) * 64);
+                        if constexpr (PD && SE) x[u] = Vw(kb + lane + (h + u) * 64);
                     }
 #pragma unroll
                     for (int u = 0; u < SPX_LDS_BATCH; ++u) {
@@ -386,6 +418,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                         if constexpr (PD) {
                             b0 = fma(vv[h + u].x, r[u].x, b0);
                             b1 = fma(vv[h + u].y, r[u].y, b1);
+                        }
+                        if constexpr (PD && SE) {
+                            d0 = fma(vv[h + u].x, x[u].x, d0);
+                            d1 = fma(vv[h + u].y, x[u].y, d1);
                         }
                     }
                 }
@@ -422,6 +458,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     const double u = fma(1.0, (i & 1) ? r.y : r.x, 0.0);
                     if (i & 1) b1 = u;
                     else b0 = u;
+                    if constexpr (SE) {
+                        const dbl2 x = Vw(k2);
+                        const double t = fma(1.0, (i & 1) ? x.y : x.x, 0.0);
+                        if (i & 1) d1 = t;
+                        else d0 = t;
+                    }
                 }
             }
         } else if (pipe && WIN && pend) {
@@ -439,6 +481,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     const dbl2 r = Rw(lane + u * 64);
                     b0 = fma(v0[u].x, r.x, b0);
                     b1 = fma(v0[u].y, r.y, b1);
+                    if constexpr (SE) {
+                        const dbl2 x = Vw(lane + u * 64);
+                        d0 = fma(v0[u].x, x.x, d0);
+                        d1 = fma(v0[u].y, x.y, d1);
+                    }
                 }
             }
             k += CH * 64;
@@ -463,7 +510,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
         } else {
             for (; k + 7 * 64 < L2; k += 8 * 64) {
-                dbl2 v[8], w[8], r[8];
+                dbl2 v[8], w[8], r[8], x[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
                 // LDS operands fetched SPX_LDS_BATCH elements at a time (one
@@ -474,6 +521,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
                         w[u] = Y(k + u * 64);
                         r[u] = Rw(k + u * 64);
+                        if constexpr (SE) x[u] = Vw(k + u * 64);
                     }
 #pragma unroll
                     for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
@@ -481,6 +529,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                         a1 = fma(v[u].y, w[u].y, a1);
                         b0 = fma(v[u].x, r[u].x, b0);
                         b1 = fma(v[u].y, r[u].y, b1);
+                        if constexpr (SE) {
+                            d0 = fma(v[u].x, x[u].x, d0);
+                            d1 = fma(v[u].y, x[u].y, d1);
+                        }
                     }
                 }
             }
@@ -492,6 +544,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 a1 = fma(v.y, w.y, a1);
                 b0 = fma(v.x, r.x, b0);
                 b1 = fma(v.y, r.y, b1);
+                if constexpr (SE) {
+                    const dbl2 x = Vw(k);
+                    d0 = fma(v.x, x.x, d0);
+                    d1 = fma(v.y, x.y, d1);
+                }
             }
         }
         }
@@ -504,19 +561,25 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 #pragma unroll
             for (int u = 0; u < CH; ++u) v0[u] = ld2<SPX_NT_A>(&cn[lane + u * 64]);
         }
-        double e, wn = 0.0;
+        double e, wn = 0.0, dd = 0.0;
         if (WIN && pend) {
             // r_tau . A_j = B_w[q,:] . A_j + sum_s U[q][s] Wt[j][s]; the window
             // terms join the lane partials before the butterflies
             double sa = fma(syl, wv, a0 + a1);
             wn = fma(uq, wv, b0 + b1);
-            wave_sum2(sa, wn);
+            if constexpr (SE) {
+                // A_j . B^-T alpha = v . A_j + sum_{s<tau} (U[:, s] . alpha) Wt[j][s]
+                dd = fma(csl, wv, d0 + d1);
+                wave_sum3(sa, wn, dd);
+            } else {
+                wave_sum2(sa, wn);
+            }
             if (lane == 0) P.Wt[j * KW + tau] = wn;
             e = fma(syp, wn, sa) - P.c[j];
         } else {
             e = wave_sum(a0 + a1) - P.c[j];
         }
-        consider(j, e, wn);
+        consider(j, e, wn, dd);
     }
     }
 
@@ -1310,7 +1373,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
             double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
             const int S = Sbc;
             const double* apd = P.A + p * L;
-            const int S2 = (S + 1) >> 1;  // dbl2 chunks
             const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
             double a[R];
 #pragma unroll
@@ -1601,6 +1663,277 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem, gridDim.x);
     else
         update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
+    stamp_tail(slot, t_tail, win);
+}
+
+// Compact-operand FTRAN pass, one B_w row per wave (the default window
+// geometry at C3 / C4: k_update<512, 1, false, true, 0, true>'s work, term for
+// term and in the same per-lane order, so the same bits).  What changes is the
+// dependency chain.  Everything that does not depend on the entering column
+// is requested at kernel entry: the pricing partials, the loop state and the
+// list size S, the column list, this row's unit flag, both alpha parities,
+// c_B / x_b / b_ixs, its U row, the first BC_PF2 chunks of its compact row
+// (chunks past S re-request chunk 0: unconditional loads, exact waits) and the
+// s_x operands.  Once p is known a single round trip remains: A_p on the
+// column list, A_p[i] and the winner's window coefficients Wt[p][.].  (In
+// k_update the chunks past the first waited for S, A_p's gather for the row
+// prefetch, and alpha for A_p's gather.)
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
+    DevState* st = P.st;
+    using Lds = UpdLds<BLOCK>;
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int NCH = BC_PF2;  // dbl2 chunks of the compact row requested at entry
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t m = P.m, L2 = P.L >> 1;
+    const int KW = P.win;
+    const int64_t i = (int64_t)blockIdx.x * WAVES + wave;  // this wave's row
+    const bool rowv = i < m;
+    const int64_t ic = rowv ? i : m - 1;
+    // ---- entry: everything independent of p (issue order = retire order)
+    const int pgi = tid < P.price_grid ? tid : P.price_grid - 1;
+    const PricePartial pwl = P.price_partials[pgi];
+    int32_t rlv[BC_RL];
+#pragma unroll
+    for (int j = 0; j < BC_RL; ++j) {
+        const int64_t c = tid + (int64_t)j * BLOCK;
+        rlv[j] = P.rlist[c < m ? c : 0];
+    }
+    const int32_t rmv = P.rmap[ic];
+    const double al0 = P.alpha0[ic], al1 = P.alpha1[ic];
+    const double cbv = P.c_B[ic], xb0 = P.x_b[ic];
+    const int64_t bix = P.b_ixs[ic];
+    const double urow = P.U[ic * KW + (lane < KW ? lane : 0)];
+    const double sxw_w = P.Wt[P.n * KW + (lane < KW ? lane : 0)];
+    struct {
+        int32_t status, nb_count, nw;
+        int64_t iter, limit, q, xb_applied;
+        double aq;
+    } Sv;
+    Sv.status = st->status;
+    Sv.nb_count = st->nb_count;
+    Sv.iter = st->iter;
+    Sv.limit = st->limit;
+    Sv.q = st->q;
+    Sv.aq = st->aq;
+    Sv.xb_applied = st->xb_applied;
+    Sv.nw = st->nw;
+    const int Sbc = P.bc_n[0];
+    const unsigned long long t_wg0 = (P.stamps && blockIdx.x == 0) ? rtime() : 0ull;
+    // the compact row's first NCH chunks (S and the state are scalars: one wait)
+    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + ic * L2;
+    dbl2 pf[NCH];
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        const int k2 = lane + 64 * t;
+        const int kk = (t == 0) ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
+        pf[t] = brow[kk];
+    }
+    const int64_t qp = Sv.q;
+    const bool pend = Sv.nw > 0;
+    const int tau = Sv.nw - 1;
+    const double sxw_u = P.U[(pend ? qp : 0) * KW + (lane < KW ? lane : 0)];
+    const double sx_x = P.xw[pend ? qp : 0];
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- entering column (v4:294-302): k_price's workgroup partials (every
+    // workgroup the same reduction), or the ranks' merged candidates
+    double min_e = INFINITY, e_enter = 0.0;
+    int64_t p = INT64_MAX;
+    int gw = 0;
+    if (P.defer_price) {
+        PricePartial w = tid < P.price_grid ? pwl : PricePartial{INFINITY, INT64_MAX, 0.0, 0.0};
+        for (int g = tid + BLOCK; g < P.price_grid; g += BLOCK) {
+            const PricePartial v = P.price_partials[g];
+            if (argmin_better(v.val, v.idx, w.val, w.idx)) w = v;
+        }
+        double bv = w.val;
+        int64_t bj = w.idx;
+        lane_argmin<64>(bv, bj);
+        bv = readlane_d(bv, 63);
+        bj = readlane_l(bj, 63);
+        const uint64_t hit = __ballot(w.val == bv && w.idx == bj);
+        const double be = readlane_d(w.pad, hit ? (int)__builtin_ctzll(hit) : 0);
+        __shared__ PricePartial s_pw[WAVES];
+        if (lane == 0) s_pw[wave] = PricePartial{bv, bj, 0.0, be};
+        lds_barrier();
+        PricePartial t = s_pw[0];
+        for (int k = 1; k < WAVES; ++k)
+            if (argmin_better(s_pw[k].val, s_pw[k].idx, t.val, t.idx)) t = s_pw[k];
+        min_e = t.val;
+        p = t.idx;
+        e_enter = t.pad;
+    } else {
+        for (int g = 0; g < P.nin; ++g) {
+            const ArgMinEntry e = P.price_in[g * P.pr_stride];
+            if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
+        }
+    }
+    if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) return;
+    wg0_mark(P, 0, t_wg0);
+    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
+    stamp_start(slot);
+    wg0_mark(P, 1, t_wg0);
+    if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
+        if (blockIdx.x == 0 && tid == 0) {
+            st->p = p;
+            st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
+            st->status = ST_OPTIMAL;
+        }
+        return;
+    }
+    // ---- the one p-dependent round trip: A_p on the list and at row i, the
+    // winner's window coefficients, the bookkeeping scalars (thread 0)
+    const double* apd = P.A + p * P.L;
+    double apv[BC_RL];
+#pragma unroll
+    for (int j = 0; j < BC_RL; ++j) apv[j] = apd[rlv[j]];
+    const double auv = apd[ic];
+    const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
+                                   : P.Wt + p * KW;
+    const double wlr = wrec[lane < KW ? lane : 0];
+    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
+    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
+    if (P.defer_price) {
+        tpre.has_e = true;
+        tpre.e_enter = e_enter;
+    }
+    const int64_t it = Sv.iter;
+    const int par = (int)(it & 1);
+    double* a_new = par ? P.alpha0 : P.alpha1;
+    const double aqp = Sv.aq;
+    const bool upd_x = Sv.xb_applied < it;
+    const double ei = (pend && rowv) ? eta_entry(par ? al1 : al0, i, qp, aqp) : 0.0;
+    unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
+    stamp_stream(win, true);
+    wg0_mark(P, 2, t_wg0);
+    // ---- compact FTRAN (as k_update BC): the unit term first (lane 0), then
+    // this lane's chunks lane + 64 t ascending, .x before .y; A_p gathered
+    // onto the list in LDS blocks of BC_APC columns
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
+    const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
+    const int S = Sbc;
+    double a = (rowv && lane == 0 && rmv < 0) ? auv : 0.0;
+    for (int cb = 0; cb < S || cb == 0; cb += BC_APC) {
+        const int ce = S < cb + BC_APC ? S : cb + BC_APC;
+        if (cb > 0) lds_barrier();  // the previous block's reads are done
+#pragma unroll
+        for (int j = 0; j < BC_RL; ++j) {
+            const int c = tid + j * BLOCK;
+            if (cb == 0 && c < ce) apc[c] = apv[j];
+        }
+        for (int c = cb + (cb == 0 ? BC_RL * BLOCK : 0) + tid; c < ce; c += BLOCK) apc[c - cb] = apd[P.rlist[c]];
+        lds_barrier();
+        const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
+        if (rowv) {
+            auto take = [&](dbl2 v, int k2) {
+                const dbl2 w = apc2[k2 - kb];
+                if (2 * k2 < S) a = fma(v.x, w.x, a);
+                if (2 * k2 + 1 < S) a = fma(v.y, w.y, a);
+            };
+            if (cb == 0) {
+#pragma unroll
+                for (int t = 0; t < NCH; ++t) {
+                    const int k2 = lane + 64 * t;
+                    if (k2 < ke) take(pf[t], k2);
+                }
+            }
+            for (int k0 = (cb == 0 ? NCH * 64 : kb); k0 < ke; k0 += 8 * 64) {
+                dbl2 v[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int k2 = k0 + lane + 64 * t;
+                    v[t] = brow[k2 < ke ? k2 : kb];
+                }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int k2 = k0 + lane + 64 * t;
+                    if (k2 < ke) take(v[t], k2);
+                }
+            }
+        }
+    }
+    // ---- window terms, the pending eta column, s_x, the basic Wt entries
+    const double wl = lane < Sv.nw ? wlr : 0.0;
+    double acc = 0.0;
+    if (rowv) {
+        const double cu = lane < tau ? urow : (lane == tau ? ei : 0.0);
+        acc = fma(cu, wl, a);
+        if (pend && lane == 0) P.U[i * KW + tau] = ei;
+    }
+    double sxw = 0.0;
+    if (pend) {
+        // (the operands masked first, the product inside the sum: the form
+        // k_update uses, so the compiler contracts it the same way)
+        const double su = lane < tau ? sxw_u : 0.0, sw = lane < tau ? sxw_w : 0.0;
+        sxw = sx_x + wave_sum(su * sw);
+        if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
+        if (lane == 0 && rowv) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
+    }
+    const double s_x = upd_x ? sxw : 0.0;
+    stamp_stream(win, false);
+    wg0_mark(P, 3, t_wg0);
+    // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partial
+    UpdPartial wp = upd_empty();
+    if (rowv) {
+        const double al = wave_sum(acc);
+        double xb = xb0;
+        if (upd_x) xb = fma(s_x, ei, xb);
+        if (lane == 0) {
+            a_new[i] = al;
+            if (upd_x) P.x_b[i] = xb;
+        }
+        const bool pos = al > P.piv_tol;
+        const double th = ratio_key(P, xb, al);
+        wp.nonpos += !pos;
+        wp.T = fma(cbv, al, wp.T);
+        if (argmin_better(th, i, wp.theta, wp.idx)) {
+            wp.theta = th;
+            wp.idx = i;
+            wp.a_w = al;
+            wp.cb_w = cbv;
+            wp.bix_w = bix;
+        }
+    }
+    UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
+    int* s_last = reinterpret_cast<int*>(smem + Lds::last);
+    if (lane == 0) red[wave] = wp;
+    lds_barrier();
+    if (P.split_tail) {  // k_tail merges after the kernel boundary
+        if (tid == 0) {
+            UpdPartial w = red[0];
+            for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
+            upd_publish(P, blockIdx.x, w);
+        }
+        return;
+    }
+    if (P.upd_tag) {  // tagged hand-off to the last workgroup
+        const uint32_t tag = (uint32_t)(it + 1);
+        if (wave == 0) {
+            UpdPartial w = red[0];
+            for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
+            upd_publish_tagged(P, blockIdx.x, w, tag, lane);
+            wg0_mark(P, 4, t_wg0);
+        }
+        if (blockIdx.x != gridDim.x - 1) return;
+        const unsigned long long t_tail = slot ? rtime() : 0;
+        update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre, tag);
+        stamp_tail(slot, t_tail, win);
+        return;
+    }
+    if (tid == 0) {
+        UpdPartial w = red[0];
+        for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
+        upd_publish(P, blockIdx.x, w);
+        drain_vmem();  // the partial is visible before the ticket
+        *s_last = arrive_last(arrive_group(P.arrive, ARR_UPDATE), gridDim.x, blockIdx.x);
+    }
+    lds_barrier();
+    if (!*s_last) return;
+    const unsigned long long t_tail = slot ? rtime() : 0;
+    update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
     stamp_tail(slot, t_tail, win);
 }
 
@@ -2182,6 +2515,11 @@ static hipError_t price_dispatch(const PriceCfg& c, const Params* P, hipStream_t
         SPX_PV(false, 2);
     }
     if (c.wm == 3) SPX_PV(false, 3);
+    if (c.wm == 4 && c.lds_y) SPX_PV(true, 4);
+    if (c.wm == 5) {
+        if (c.lds_y) SPX_PV(true, 5);
+        SPX_PV(false, 5);
+    }
 #undef SPX_PV
     return hipErrorInvalidValue;
 }
@@ -2228,13 +2566,32 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
     return hipGetLastError();
 }
 
+template <int BLOCK>
+static hipError_t launch_ftran_bc(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    const size_t lds = UpdLds<BLOCK>::bytes + (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8;
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    if (e0 || e1)
+        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+    else
+        hipLaunchKernelGGL((k_ftran_bc<BLOCK>), dim3(grid), dim3(BLOCK), lds, s, P);
+    return hipGetLastError();
+}
+
 template <int BLOCK, int R>
-static hipError_t launch_update_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+static hipError_t launch_update_t(const Params& P, int grid, bool bc_entry, hipStream_t s, hipEvent_t e0,
+                                  hipEvent_t e1) {
     if (P.row_shard) return launch_update_k<BLOCK, R, true, false>(P, grid, s, e0, e1);
     if (!P.win) return launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
     // B_w loads: default policy while B_w fits the Infinity Cache beside the
     // window state (spx_common.h SPX_NT_BWIN), non-temporal beyond
-    if (P.bc) return launch_update_k<BLOCK, R, false, true, 0, true>(P, grid, s, e0, e1);  // compact FTRAN
+    if (P.bc) {  // compact FTRAN
+        if (R == 1 && bc_entry) return launch_ftran_bc<BLOCK>(P, grid, s, e0, e1);
+        return launch_update_k<BLOCK, R, false, true, 0, true>(P, grid, s, e0, e1);
+    }
     if (win_b_cached(P)) return launch_update_k<BLOCK, R, false, true, 0>(P, grid, s, e0, e1);
     return launch_update_k<BLOCK, R, false, true, 1>(P, grid, s, e0, e1);
 }
@@ -2390,11 +2747,11 @@ hipError_t launch_finalize_rs(const Params& P, hipStream_t s) {
 template <int BLOCK>
 static hipError_t launch_update_b(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (c.rows) {
-        case 1: return launch_update_t<BLOCK, 1>(P, c.grid, s, e0, e1);
-        case 2: return launch_update_t<BLOCK, 2>(P, c.grid, s, e0, e1);
-        case 4: return launch_update_t<BLOCK, 4>(P, c.grid, s, e0, e1);
+        case 1: return launch_update_t<BLOCK, 1>(P, c.grid, c.bc_entry != 0, s, e0, e1);
+        case 2: return launch_update_t<BLOCK, 2>(P, c.grid, c.bc_entry != 0, s, e0, e1);
+        case 4: return launch_update_t<BLOCK, 4>(P, c.grid, c.bc_entry != 0, s, e0, e1);
         case 8:
-            if constexpr (BLOCK <= 512) return launch_update_t<BLOCK, 8>(P, c.grid, s, e0, e1);
+            if constexpr (BLOCK <= 512) return launch_update_t<BLOCK, 8>(P, c.grid, c.bc_entry != 0, s, e0, e1);
             break;
     }
     return hipErrorInvalidValue;
@@ -2429,6 +2786,111 @@ hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n
     hipLaunchKernelGGL(k_generate, dim3(grid_for(L * n, 256) * 4), dim3(256), 0, s, A, b, c, m, n, L, seed);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Steepest-edge pricing (SPX_PRICING_STEEPEST; oracle se_choose).  Weights
+// gamma_j = 1 + ||B^-1 A_j||^2: exact at the slack basis (k_se_init), then
+// kept by the Goldfarb-Reid recurrence inside k_price, which needs for the
+// pending pivot (alpha = its FTRAN column, a_prev of the coming pass; B^-1
+// before it = B_w + sum_{s<tau} eta_s r_s^T):
+//   A_j . B^-T alpha = (B_w^T alpha) . A_j + sum_{s<tau} (U[:, s] . alpha) Wt[j][s]
+// and gamma_p = 1 + ||alpha||^2.  k_se_part / k_se_fin form those before each
+// pricing pass (after any fold): the column sums of M^T alpha for M = [B_w's
+// columns (the compact list, or all of B_w) | U | alpha], per row block in
+// ascending row order, then over the blocks in ascending order.
+// ---------------------------------------------------------------------------
+constexpr int SE_RB = 64;  // rows per k_se_part workgroup
+
+__device__ __forceinline__ bool se_pending(const Params& P, int& nw, const double*& al) {
+    const DevState* st = P.st;
+    if (st->status != ST_RUNNING || st->iter >= st->limit) return false;
+    nw = st->nw;
+    al = (st->iter & 1) ? P.alpha1 : P.alpha0;  // alpha of the pending pivot
+    return nw > 0;
+}
+
+__global__ __launch_bounds__(256) void k_se_part(Params P) {
+    int nw;
+    const double* al;
+    if (!se_pending(P, nw, al)) return;
+    const int64_t m = P.m, L = P.L;
+    const int KW = P.win, tau = nw - 1;
+    const int S = P.bc ? P.bc_n[0] : (int)m;
+    const int ncols = S + KW + 1;
+    const int64_t i0 = (int64_t)blockIdx.x * SE_RB;
+    const int nr = (int)(m - i0 < SE_RB ? m - i0 : SE_RB);
+    __shared__ double sa[SE_RB];
+    if (threadIdx.x < SE_RB) sa[threadIdx.x] = threadIdx.x < nr ? al[i0 + threadIdx.x] : 0.0;
+    __syncthreads();
+    const double* Mw = P.bc ? P.bc : P.B0;
+    double* out = P.se_part + (int64_t)blockIdx.x * (L + KW + 1);
+    for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+        double acc = 0.0;
+        if (c < S) {
+            for (int r = 0; r < nr; ++r) acc = fma(Mw[(i0 + r) * L + c], sa[r], acc);
+        } else if (c < S + KW) {
+            const int sc = c - S;
+            if (sc < tau)
+                for (int r = 0; r < nr; ++r) acc = fma(P.U[(i0 + r) * KW + sc], sa[r], acc);
+        } else {
+            for (int r = 0; r < nr; ++r) acc = fma(sa[r], sa[r], acc);
+        }
+        out[c] = acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_se_fin(Params P) {
+    int nw;
+    const double* al;
+    if (!se_pending(P, nw, al)) return;
+    const int64_t m = P.m, L = P.L;
+    const int KW = P.win;
+    const int S = P.bc ? P.bc_n[0] : (int)m;
+    const int ncols = S + KW + 1;
+    const int64_t stride = L + KW + 1;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = t0; c < ncols; c += nt) {
+        double v = 0.0;
+        for (int g = 0; g < P.se_parts; ++g) v += P.se_part[g * stride + c];
+        if (c < S) P.se_v[P.bc ? (int64_t)P.rlist[c] : c] = v;
+        else if (c < S + KW) P.se_cg[c - S] = v;
+        else P.se_cg[KW] = 1.0 + v;
+    }
+    if (P.bc)  // the unit columns of B_w: (B_w^T alpha)_k = alpha_k
+        for (int64_t k = t0; k < m; k += nt)
+            if (P.rmap[k] < 0) P.se_v[k] = al[k];
+}
+
+// gamma_j = 1 + ||A_j||^2 for every column (the slack basis B = I), one wave
+// per column, lane-strided then a butterfly
+__global__ __launch_bounds__(256) void k_se_init(Params P) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = w0; j < P.n; j += nwv) {
+        const double* col = P.A + j * P.L;
+        double a = 0.0;
+        for (int64_t k = lane; k < P.m; k += 64) a = fma(col[k], col[k], a);
+        a = wave_sum(a);
+        if (lane == 0) P.W[j] = 1.0 + a;
+    }
+}
+
+hipError_t launch_se_init(const Params& P, hipStream_t s) {
+    if (!P.steep) return hipSuccess;
+    hipLaunchKernelGGL(k_se_init, dim3(grid_for(P.n * 64, 256)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_se_prep(const Params& P, hipStream_t s) {
+    if (!P.steep) return hipSuccess;
+    hipLaunchKernelGGL(k_se_part, dim3((unsigned)P.se_parts), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_se_fin, dim3(grid_for(P.L + P.win + 1, 256)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+int se_parts_for(int64_t m) { return (int)((m + SE_RB - 1) / SE_RB); }
 
 hipError_t launch_reset(const Params& P, hipStream_t s) {
     const int64_t w = P.m > P.n ? P.m : P.n;

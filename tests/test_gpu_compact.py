@@ -175,3 +175,20 @@ def test_compact_partial_last_wave(spx, rows, m, n, window):
         assert np.array_equal(a[1][key], one[1][key]), key  # alpha has the per-lane order of R = 1
     assert a[3].status == d[3].status and a[3].pivots == d[3].pivots
     assert abs(a[3].z - d[3].z) <= 1e-9 * max(1.0, abs(d[3].z))
+
+
+@pytest.mark.parametrize("kw", [dict(m=401, n=1604, seed=11, window=64), dict(m=400, n=1600, seed=2, window=16),
+                                dict(m=1024, n=4096, seed=0, window=64), dict(m=300, n=1200, seed=8, window=32, pricing=1),
+                                dict(m=257, n=1001, seed=6, window=16, ratio_test=2)],
+                         ids=["m401-w64", "m400-w16", "m1024-w64", "devex", "harris"])
+def test_compact_entry_kernel_same_bits(spx, kw):
+    """k_ftran_bc (the one-row-per-wave compact pass with every p-independent
+    load at kernel entry) against k_update<..., BC> (SPX_FTRAN_BC_ENTRY=0):
+    the same arithmetic in the same order, so the same bits everywhere."""
+    a = _run(spx, False, 200, persist=False, **kw)
+    with _env(SPX_FTRAN_BC_ENTRY="0"):
+        b = _run(spx, False, 200, persist=False, **kw)
+    assert np.array_equal(a[2], b[2])
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    assert a[3].pivots == b[3].pivots and a[3].z == b[3].z

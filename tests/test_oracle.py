@@ -194,3 +194,53 @@ def test_devex_reaches_optimum(oracle, golden):
     x = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED, pricing=oracle.PRICING_DEVEX)
     assert abs(x.z - z_star) <= 1e-9 * abs(z_star)
     assert x.pivots < d.pivots  # Devex needs fewer pivots on this degenerate LP (347 vs 1124)
+
+
+def _exact_se_weights(A, basis, binv):
+    """gamma_j = 1 + ||B^-1 A_j||^2 for the non-basic columns (the definition)."""
+    n = A.shape[0]
+    bs = set(int(j) for j in basis)
+    nb = np.array([j for j in range(n) if j not in bs])
+    return nb, 1.0 + np.sum((binv @ A[nb].T) ** 2, axis=0)
+
+
+@pytest.mark.parametrize("m,n,seed,k", [(120, 480, 1, 30), (200, 800, 3, 60), (160, 640, 7, 100)])
+def test_steepest_edge_recurrence_is_exact(oracle, m, n, seed, k):
+    """The Goldfarb-Reid recurrence (se_choose) keeps the exact weights: after
+    k steepest-edge pivots they equal 1 + ||B^-1 A_j||^2 from the final B^-1
+    within 1e-10 (relative)."""
+    A, b, c = oracle.generate(m, n, seed)
+    r = oracle.solve(A, b, c, pricing=oracle.PRICING_STEEPEST, max_iter=k, want_state=True)
+    assert r.pivots >= min(k, 30)
+    nb, ex = _exact_se_weights(A, r.b_ixs, r.binv)
+    assert np.max(np.abs(r.weights[nb] - ex) / ex) <= 1e-10
+
+
+def test_steepest_edge_reaches_optimum(oracle, golden):
+    """Steepest edge reaches the HiGHS optima (golden cases; a degenerate LP
+    with the guarded ratio test), with fewer pivots than Dantzig and Devex on
+    the degenerate LP."""
+    from lpgen import degenerate_lp, highs_opt
+
+    for case in golden["cases"][:9]:
+        A, b, c = oracle.generate(case["m"], case["n"], case["seed"])
+        r = oracle.solve(A, b, c, pricing=oracle.PRICING_STEEPEST)
+        assert r.status == oracle.OPTIMUM_FOUND
+        assert abs(r.z - case["highs_z"]) <= 1e-9 * abs(case["highs_z"])
+        assert sorted(int(j) for j in r.b_ixs) == case["highs_basis"]
+    A, b, c = degenerate_lp(300, 900, 4)
+    z_star = highs_opt(A, b, c)
+    d = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED)
+    x = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED, pricing=oracle.PRICING_DEVEX)
+    s = oracle.solve(A, b, c, ratio=oracle.RATIO_GUARDED, pricing=oracle.PRICING_STEEPEST)
+    assert s.status == oracle.OPTIMUM_FOUND and abs(s.z - z_star) <= 1e-9 * abs(z_star)
+    assert s.pivots < d.pivots and s.pivots <= x.pivots
+
+
+def test_steepest_edge_refactor_keeps_weights(oracle):
+    """Reinversion changes B^-1's bits, not the weights' recurrence: the same
+    optimum, weights still exact."""
+    A, b, c = oracle.generate(150, 450, 3)
+    r = oracle.solve(A, b, c, pricing=oracle.PRICING_STEEPEST, refactor_every=20, want_state=True, max_iter=70)
+    nb, ex = _exact_se_weights(A, r.b_ixs, r.binv)
+    assert np.max(np.abs(r.weights[nb] - ex) / ex) <= 1e-10

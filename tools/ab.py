@@ -1,6 +1,6 @@
 """A/B of Context keyword variants on one LP: graph-mode ms per pivot, variants
 interleaved over several rounds.
-    python tools/ab.py --variants '[{}, {"counted_tail": true}]' [--m 4096 --n 16384 --k 252 --rounds 4]"""
+    python tools/ab.py --variants '[{}, {"counted_tail": true}, {"_env": {"SPX_FTRAN_BC_ENTRY": "0"}}]' [--m 4096 --n 16384 --k 252 --rounds 4]"""
 import argparse
 import json
 import os
@@ -19,7 +19,23 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--variants", default='[{}]')
 a = ap.parse_args()
 vs = json.loads(a.variants)
-ctxs = [spx.Context(m=a.m, n=a.n, seed=0, device=0, **kw) for kw in vs]
+def make(kw):
+    # "_env": environment read by spx_create (e.g. SPX_FTRAN_BC_ENTRY=0), set only while creating
+    kw = dict(kw)
+    env = kw.pop("_env", {})
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return spx.Context(m=a.m, n=a.n, seed=0, device=0, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+ctxs = [make(kw) for kw in vs]
 for c in ctxs:
     c.iterate(a.warm)
 res = [[] for _ in vs]

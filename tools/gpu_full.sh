@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full GPU check for one round step: every -m gpu test, smoke(), the default
-# bench line, and the C3 phase probe.  usage: tools/r02_full.sh TAG
+# bench line, and the C3 phase probe.  usage: tools/gpu_full.sh TAG
 set -o pipefail
 T=${1:-full}
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"

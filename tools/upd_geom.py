@@ -21,7 +21,7 @@ def rate(**kw):
         return best, ctx.config()
 
 
-for blk, rows in [(512, 1), (256, 1), (1024, 1), (512, 2), (256, 2), (512, 4), (256, 4), (1024, 4)]:
+for blk, rows in [(512, 1), (256, 1), (1024, 1), (512, 2), (1024, 2), (256, 4), (512, 4), (1024, 4), (256, 8), (512, 8)]:
     try:
         r, cfg = rate(update_block=blk, update_rows=rows)
         print(json.dumps({"update_block": blk, "update_rows": rows, "it_s": round(r, 1),
