@@ -370,8 +370,10 @@ int spx_ftran_cols(spx_ctx* ctx, int32_t* cols);
  * launches, [4] passes inside them, [5] eta-window folds (k_fold) enqueued,
  * [6] the window position (pivots since the last fold + 1; a fold is due
  * before the next pass when it equals [7]), [7] the window size KW (0 =
- * explicit B^-1). */
-#define SPX_DISPATCH_FIELDS 8
+ * explicit B^-1), [8] persistent launches whose grid was found not
+ * co-resident (another stream or process held CUs; the context then
+ * switched to two-kernel passes and made those pivots that way). */
+#define SPX_DISPATCH_FIELDS 9
 int spx_dispatch_stats(spx_ctx* ctx, int64_t out[SPX_DISPATCH_FIELDS]);
 
 /* Host-only helpers (no device needed), shared with the device code:

@@ -341,10 +341,10 @@ class Context:
 
     def dispatch_stats(self):
         """Monotone counts of what the loop enqueued (spx_dispatch_stats)."""
-        out = (ctypes.c_int64 * 8)()
+        out = (ctypes.c_int64 * 9)()
         check(self._L.spx_dispatch_stats(self._h, out))
         keys = ("eager_passes", "graph_launches", "graph_passes", "persistent_launches", "persistent_passes",
-                "folds", "window_pos", "window")
+                "folds", "window_pos", "window", "persist_fallbacks")
         return dict(zip(keys, list(out)))
 
     def config(self):

@@ -138,6 +138,7 @@ struct spx_ctx {
     int nw = 0;  // eta window: device st->nw as of the last readback, advanced per enqueued pass
     // what the loop actually enqueued (spx_dispatch_stats)
     int64_t n_eager = 0, n_graph_launch = 0, n_graph_pass = 0, n_persist_launch = 0, n_persist_pass = 0;
+    int64_t n_persist_fallback = 0;  // persistent launches found not co-resident
     int64_t n_folds = 0;
     int graph_folds = 0;     // folds inside one captured batch
     bool capturing = false;  // build_graph: passes are recorded, not run
@@ -775,6 +776,7 @@ int iterate(spx_ctx* x, int64_t k) {
 
 // Persistent loop: one launch per window (k_loop, co-resident grid), folds between.
 int iterate_persist(spx_ctx* x, int64_t k) {
+    const int64_t target = x->pivots + k;
     int64_t left = k;
     while (left > 0) {
         const bool fold = fold_due(x);
@@ -794,7 +796,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
         a.npasses = (int32_t)np;
         a.epoch = ++x->loop_epoch & 0x1ffffffu;  // 25 bits: the tag keeps 7 for pass and phase
         if (!x->timing) a.clock = nullptr;
-        HIP_TRY(hipMemsetAsync(a.ls, 0, sizeof(LoopState), x->stream));
+        HIP_TRY(hipMemsetAsync(a.ls, 0, LOOP_STATE_RESET, x->stream));
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (x->timing) {
             if (x->ev_loop.size() < 2 * (x->n_loop + 1)) {
@@ -835,6 +837,19 @@ int iterate_persist(spx_ctx* x, int64_t k) {
     SPX_TRY(read_state(x));
     LoopState ls{};
     HIP_TRY(hipMemcpy(&ls, x->la.ls, sizeof(ls), hipMemcpyDeviceToHost));
+    if (ls.nores) {
+        // some launch found its grid not co-resident (another stream or
+        // process held CUs) and left the state untouched: from here on this
+        // context runs two-kernel passes, and the passes those launches did
+        // not make are made that way now
+        HIP_TRY(hipMemsetAsync(x->la.ls, 0, sizeof(LoopState), x->stream));
+        x->persist = false;
+        ++x->n_persist_fallback;
+        x->nw = x->P.win ? x->st_host->nw : 0;
+        const int64_t left = target - x->pivots;
+        if (x->status == SPX_STATUS_MAX_ITER && left > 0) return iterate_raw(x, left);
+        return SPX_OK;
+    }
     if (ls.err) return fail(SPX_ERR_STATE, "persistent loop: a grid barrier timed out");
     return SPX_OK;
 }
@@ -1520,6 +1535,7 @@ int spx_dispatch_stats(spx_ctx* x, int64_t out[SPX_DISPATCH_FIELDS]) {
     out[5] = x->n_folds;
     out[6] = x->P.win ? x->nw : 0;
     out[7] = x->P.win;
+    out[8] = x->n_persist_fallback;
     return SPX_OK;
 }
 

@@ -56,6 +56,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 // two butterflies interleaved (their cross-lane latencies overlap)
+// a * b rounded on its own: no fma contraction into the sum it feeds (the
+// compiler's fp-contract=fast would otherwise fuse it into the first butterfly
+// add in some kernels and not in others, and a product that is fused differs
+// in the last bit from one that is not)
+__device__ __forceinline__ double mul_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+
 __device__ __forceinline__ void wave_sum3(double& a, double& b, double& c) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

@@ -1462,7 +1462,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         }
         double sxw = 0.0;
         if (pend) {
-            sxw = sx_x + wave_sum(sx_u * sx_w);
+            sxw = sx_x + wave_sum(mul_nc(sx_u, sx_w));
             if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
             if (lane == 0) {
                 // the exact Wt entries of the basic columns for the pending
@@ -1865,10 +1865,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     }
     double sxw = 0.0;
     if (pend) {
-        // (the operands masked first, the product inside the sum: the form
-        // k_update uses, so the compiler contracts it the same way)
-        const double su = lane < tau ? sxw_u : 0.0, sw = lane < tau ? sxw_w : 0.0;
-        sxw = sx_x + wave_sum(su * sw);
+        sxw = sx_x + wave_sum(lane < tau ? mul_nc(sxw_u, sxw_w) : 0.0);
         if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
         if (lane == 0 && rowv) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
     }
@@ -1999,7 +1996,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
     // s_x = r_tau . b = xw[q] + sum_{s<tau} U[q][s] Wt[n][s] (v4:347), as k_update
     double sxw = 0.0;
     if (pend) {
-        sxw = lane < tau ? P.U[qp * KW + lane] * P.Wt[P.n * KW + lane] : 0.0;
+        sxw = lane < tau ? mul_nc(P.U[qp * KW + lane], P.Wt[P.n * KW + lane]) : 0.0;
         sxw = P.xw[qp] + wave_sum(sxw);
         if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
     }

@@ -29,11 +29,17 @@
 namespace spx {
 
 struct alignas(16) LoopState {
-    uint32_t bar;   // grid barrier counter (zeroed before every launch)
-    int32_t err;    // 1: a barrier timed out
-    int32_t passes; // passes completed by this launch
-    int32_t pad;
+    uint32_t bar;    // grid barrier counter (zeroed before every launch)
+    int32_t err;     // 1: a barrier timed out; 2: the grid was not co-resident
+    int32_t passes;  // passes completed by this launch
+    uint32_t arrive; // workgroups that reached the entry check (grid_arrive)
+    // not zeroed per launch: launches whose grid was not all resident
+    // (another kernel or process held CUs), read and cleared by the host
+    int32_t nores;
+    int32_t pad[3];
 };
+// bytes of LoopState reset before every launch
+constexpr size_t LOOP_STATE_RESET = 16;
 
 struct LoopArgs {
     PricePartial* pp;           // G pricing partials
@@ -61,5 +67,8 @@ struct LoopCfg {
 // cannot hold one workgroup per CU.
 hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c, bool want_bc = false);
 hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s);
+
+// the grid a persistent launch uses (SPX_LOOP_OVERSUB=1: twice it, for tests)
+int loop_grid_launched(int grid);
 
 }  // namespace spx

@@ -6,6 +6,7 @@
 // grouped by this launch's geometry.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "spx_common.h"
 #include "spx_loop.h"
@@ -210,6 +211,8 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
     double* rs = ys + (LDS_R ? L : 0);
     Sh& S = *reinterpret_cast<Sh*>(smem + (LDS_R ? 2 : 1) * L * 8);
     __shared__ int s_ok;
+    // the whole grid resident, or nobody touches the state (spx_grid.h)
+    if (!grid_arrive(La.ls, &s_ok)) return;
 
     // ---- launch prologue: the state every workgroup keeps (uniform)
     int64_t it = st->iter;
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
             const double wl = lane < nw ? ld_agent(&P.Wt[p * KW + lane]) : 0.0;
             double sxw = 0.0;
             if (pend) {
-                sxw = lane < tau ? ld_agent(&P.U[q * KW + lane]) * ld_agent(&P.Wt[n * KW + lane]) : 0.0;
+                sxw = lane < tau ? mul_nc(ld_agent(&P.U[q * KW + lane]), ld_agent(&P.Wt[n * KW + lane])) : 0.0;
                 sxw = P.xw[q] + wave_sum(sxw);
                 if (wg0 && tid == 0) st_agent(&P.Wt[n * KW + tau], sxw);
             }
@@ -690,7 +693,16 @@ hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hip
     // loop_prepare) is co-resident without the cooperative launch's check,
     // and the grid barrier is our own (spx_grid.h), so no cooperative queue
     // (MI355X_MICROARCH.md coop-launch: +15-19 us host wall per launch)
-    return hipLaunchKernel(fn, dim3(c.grid), dim3(c.block), args, (size_t)c.lds_bytes, s);
+    return hipLaunchKernel(fn, dim3(loop_grid_launched(c.grid)), dim3(c.block), args, (size_t)c.lds_bytes, s);
+}
+
+// SPX_LOOP_OVERSUB=1 (tests): launch 4,096 more workgroups than the
+// co-resident grid -- more than any GPU holds at once (at most 32 waves per
+// CU) -- so the entry check (grid_arrive) must fail and the host fall back to
+// two-kernel passes
+int loop_grid_launched(int grid) {
+    const char* v = std::getenv("SPX_LOOP_OVERSUB");
+    return (v && v[0] == '1') ? grid + 4096 : grid;
 }
 
 }  // namespace spx

@@ -19,6 +19,7 @@
 
 #include "spx_common.h"
 #include "spx_fold.h"
+#include "spx_grid.h"
 #include "spx_loop.h"
 #include "spx_tableau.h"
 #include "spx_tabdev.h"
@@ -462,6 +463,10 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
     const bool wg0 = blockIdx.x == 0;
     const int64_t L = P.L, m = P.m, n = P.n;
     const int KW = P.win;
+    {  // the whole grid resident, or nobody touches the state (spx_grid.h)
+        __shared__ int s_arr;
+        if (!grid_arrive(La.ls, &s_arr)) return;
+    }
 
     int64_t it = st->iter;
     const int64_t it0 = it;
@@ -640,7 +645,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_loop(Params P, LoopArgs La, int c
         lds_barrier();
         // s_x = r_tau . b for phase B's x_b update (k_tab_update's formula)
         double sxw = 0.0;
-        if (pend) sxw = xwq + wave_sum(lane < tau ? S.Uq[lane] * wtn : 0.0);
+        if (pend) sxw = xwq + wave_sum(lane < tau ? mul_nc(S.Uq[lane], wtn) : 0.0);
         TAB_STAMP(1);
         TabPick best{INFINITY, INT64_MAX, 0.0, 0.0, -1};
         double cw = 0.0, cwt = 0.0;  // this column's window entry and Devex weight, stored in phase B
@@ -1111,8 +1116,8 @@ hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c,
     void* args[] = {const_cast<Params*>(&P), const_cast<LoopArgs*>(&a), &cpw, &rw};
     // plain launch of a co-resident grid (c.grid <= CUs, per_cu >= 1): the
     // barriers and hand-offs are our own, see launch_loop
-    return hipLaunchKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(c.grid), dim3(c.block), args,
-                           (size_t)c.lds_bytes, s);
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(loop_grid_launched(c.grid)),
+                           dim3(c.block), args, (size_t)c.lds_bytes, s);
 }
 
 }  // namespace spx

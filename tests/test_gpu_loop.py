@@ -100,3 +100,27 @@ def test_loop_auto_on_large_m(spx):
         assert ctx.config()["persistent"] == 1 and ctx.ftran_cols() == 0
     with spx.Context(m=12000, n=13000, seed=0, window=64, persist=False) as ctx:
         assert ctx.config()["persistent"] == 0 and ctx.ftran_cols() == 0
+
+
+@pytest.mark.parametrize("tableau", [False, True], ids=["k_loop", "k_tab_loop"])
+def test_loop_not_coresident_falls_back(spx, oracle, monkeypatch, tableau):
+    """A persistent launch whose grid is not all resident (SPX_LOOP_OVERSUB=1
+    launches 4,096 workgroups more than the co-resident grid) must not hang in a grid barrier:
+    the entry check (spx_grid.h grid_arrive) sends every workgroup home
+    within 2 ms without touching the state, and the context makes those
+    pivots as two-kernel passes -- the oracle's pivots and optimum."""
+    m, n, seed = 300, 900, 3
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, eps=1e-7, trace_cap=4096)
+    monkeypatch.setenv("SPX_LOOP_OVERSUB", "1")
+    with spx.Context(A, b, c, eps=1e-7, window=16, persist=True, tableau=tableau, trace=4096) as ctx:
+        assert ctx.config()["persistent"] == 1
+        st, piv = ctx.iterate(50)
+        assert piv == 50
+        ds = ctx.dispatch_stats()
+        assert ds["persist_fallbacks"] >= 1 and ctx.config()["persistent"] == 0
+        r = ctx.solve()
+        tp, tq = ctx.trace()
+    assert r.status == spx.SolveStatus.OptimumFound and r.pivots == ref.pivots
+    assert list(tp) == list(ref.trace_p) and list(tq) == list(ref.trace_q)
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
