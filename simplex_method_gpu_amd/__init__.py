@@ -295,6 +295,16 @@ class Context:
         return {"price_ms": tp.value, "price_launches": np_.value,
                 "update_ms": tu.value, "update_launches": nu.value}
 
+    def wg_times(self):
+        """Per-workgroup clock of the last compact FTRAN launch (stamps=True):
+        array (grid, 4) of 100 MHz ticks at entry, p known, alpha formed,
+        partial published (spx_wg_times)."""
+        cap = 4 * 8192
+        out = np.zeros(cap, dtype=np.uint64)
+        cnt = ctypes.c_int64()
+        check(self._L.spx_wg_times(self._h, _ptr(out), cap, ctypes.byref(cnt)))
+        return out[: 4 * cnt.value].reshape(cnt.value, 4)
+
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""
         out = (ctypes.c_double * 18)()

@@ -508,7 +508,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // upload), while A_p's gather fits beside the k_update LDS
     x->bc_want = bc_possible(x, P) && (!x->persist || x->lcfg.bc_lds > 0);
     if (x->opts.flags & SPX_FLAG_STAMPS) {
-        SPX_TRY(x->alloc(&P.stamps, 32));
+        SPX_TRY(x->alloc(&P.stamps, (size_t)(32 + 4 * std::max<int64_t>(uc.grid, 1))));
         SPX_TRY(reset_stamps(x));
     }
     SPX_TRY(x->alloc(&x->send, (size_t)P.pr_stride));
@@ -1399,6 +1399,16 @@ int spx_get_trace(spx_ctx* x, int64_t* p, int64_t* q, int64_t cap, int64_t* coun
         if (q) q[i] = buf[2 * i + 1];
     }
     if (count) *count = k;
+    return SPX_OK;
+}
+
+int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    const int64_t k = std::min<int64_t>(cap, 4 * (int64_t)x->ucfg.grid);
+    if (k > 0) HIP_TRY(hipMemcpy(out, x->P.stamps + 32, sizeof(uint64_t) * (size_t)k, hipMemcpyDeviceToHost));
+    if (count) *count = x->ucfg.grid;
     return SPX_OK;
 }
 

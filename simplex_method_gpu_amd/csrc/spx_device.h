@@ -273,11 +273,13 @@ struct Params {
     // B_w by its non-unit columns (eta window, two-kernel passes; DESIGN.md
     // §4a "compact FTRAN").  With A[:, ns:] = I, column k of B_w is e_k while
     // slack k has stayed basic in row k, so B_w = I + (columns rlist[0..S)).
-    // bc: m x L, row i's first S entries = B_w[i][rlist[c]] (gathered after
+    // bc: m rows at pitch bc_n[1] (S rounded up to 64; the allocation is m x
+    // L), row i's first S entries = B_w[i][rlist[c]] (gathered after
     // every fold from the dense B_w, which stays the master copy); rmap[k] =
     // c or -1 (unit column); rleft[k] = 1 once row k has been a leaving row
     // (or, after a reinversion, when slack k is not basic in row k): a
-    // superset of the non-unit columns; bc_n[0] = S.  nullptr: dense FTRAN.
+    // superset of the non-unit columns; bc_n[0] = S, bc_n[1] = the row pitch.
+    // nullptr: dense FTRAN.
     double* bc;
     int32_t* rlist;
     int32_t* rmap;

@@ -1126,11 +1126,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         // (each row clamped on its own: in a partly filled last wave, row u <
         // nvalid must be row pf_row + u, which the compact path consumes)
         const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? P.bc : P.B0);
+        const int64_t ld2r = BC ? (int64_t)(P.bc_n[1] >> 1) : L2c;  // row pitch (compact: bc_pitch)
 #pragma unroll
         for (int t = 0; t < PFU; ++t) {
             const int64_t k = (BC && t >= BC_PF) ? lane : (lane + t * 64 < L2c ? lane + t * 64 : L2c - 1);
 #pragma unroll
-            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[clamp_row(pf_row + u, P.m) * L2c + k]);
+            for (int u = 0; u < R; ++u) pfb[t][u] = ld2<BNT>(&b0[clamp_row(pf_row + u, P.m) * ld2r + k]);
         }
     }
     // compact FTRAN: the column list and this wave's unit flags, ahead of p
@@ -1245,13 +1246,14 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if constexpr (BC) {
         Sbc = P.bc_n[0];
         const int64_t L2c = P.L >> 1;
+        const int64_t ld2r = P.bc_n[1] >> 1;
         const dbl2* b0 = reinterpret_cast<const dbl2*>(P.bc);
 #pragma unroll
         for (int t = BC_PF; t < BC_PF2; ++t) {
             const int k2 = lane + 64 * t;
             const int kk = (2 * k2 < Sbc && k2 < L2c) ? k2 : lane;
 #pragma unroll
-            for (int u = 0; u < R; ++u) pf2[t - BC_PF][u] = b0[clamp_row(pf_row + u, P.m) * L2c + kk];
+            for (int u = 0; u < R; ++u) pf2[t - BC_PF][u] = b0[clamp_row(pf_row + u, P.m) * ld2r + kk];
         }
         const double* apd = P.A + p * P.L;
 #pragma unroll
@@ -1393,7 +1395,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     if (u < nvalid) {
-                        const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * L2;
+                        const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * (int64_t)(P.bc_n[1] >> 1);
                         auto take = [&](dbl2 v, int k2) {
                             const dbl2 w = apc2[k2 - kb];
                             if (2 * k2 < S) a[u] = fma(v.x, w.x, a[u]);
@@ -1721,9 +1723,11 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     Sv.xb_applied = st->xb_applied;
     Sv.nw = st->nw;
     const int Sbc = P.bc_n[0];
+    const int64_t ldc = P.bc_n[1];  // compact row pitch (k_bc_list)
     const unsigned long long t_wg0 = (P.stamps && blockIdx.x == 0) ? rtime() : 0ull;
+    const unsigned long long t_wg_entry = P.stamps ? rtime() : 0ull;
     // the compact row's first NCH chunks (S and the state are scalars: one wait)
-    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + ic * L2;
+    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + ic * ldc);
     dbl2 pf[NCH];
 #pragma unroll
     for (int t = 0; t < NCH; ++t) {
@@ -1775,6 +1779,11 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
     stamp_start(slot);
     wg0_mark(P, 1, t_wg0);
+    unsigned long long* const wgt = (P.stamps && tid == 0) ? P.stamps + 32 + 4 * (int64_t)blockIdx.x : nullptr;
+    if (wgt) {
+        wgt[0] = t_wg_entry;
+        wgt[1] = rtime();
+    }
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
@@ -1785,10 +1794,12 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     }
     // ---- the one p-dependent round trip: A_p on the list and at row i, the
     // winner's window coefficients, the bookkeeping scalars (thread 0)
+    // (only the S list slots: every workgroup gathers the same column, so
+    // slots past S would multiply the L2 requests for nothing)
     const double* apd = P.A + p * P.L;
     double apv[BC_RL];
 #pragma unroll
-    for (int j = 0; j < BC_RL; ++j) apv[j] = apd[rlv[j]];
+    for (int j = 0; j < BC_RL; ++j) apv[j] = (tid + j * BLOCK < Sbc) ? apd[rlv[j]] : 0.0;
     const double auv = apd[ic];
     const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
                                    : P.Wt + p * KW;
@@ -1872,6 +1883,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     const double s_x = upd_x ? sxw : 0.0;
     stamp_stream(win, false);
     wg0_mark(P, 3, t_wg0);
+    if (wgt) wgt[2] = rtime();
     // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partial
     UpdPartial wp = upd_empty();
     if (rowv) {
@@ -1913,6 +1925,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
             upd_publish_tagged(P, blockIdx.x, w, tag, lane);
             wg0_mark(P, 4, t_wg0);
+            if (wgt) wgt[3] = rtime();
         }
         if (blockIdx.x != gridDim.x - 1) return;
         const unsigned long long t_tail = slot ? rtime() : 0;
@@ -2653,16 +2666,23 @@ __global__ __launch_bounds__(1024) void k_bc_list(Params P) {
         if (tid == 0) s_base += tot;
         __syncthreads();
     }
-    if (tid == 0) P.bc_n[0] = s_base;
+    if (tid == 0) {
+        P.bc_n[0] = s_base;
+        // row pitch of bc: S rounded up to 64 doubles (512 B).  Rows then lie
+        // back to back (m x pitch, contiguous), so a wave's rows spread over
+        // the HBM channels; at the full pitch L every row started a multiple
+        // of L * 8 bytes apart
+        P.bc_n[1] = s_base > 0 ? ((s_base + 63) / 64) * 64 : 64;
+    }
 }
 constexpr int BC_ROWS = 4;  // rows per k_bc_gather workgroup
 __global__ __launch_bounds__(256) void k_bc_gather(Params P) {
     const int S = P.bc_n[0];
-    const int64_t L = P.L;
+    const int64_t L = P.L, ldc = P.bc_n[1];
     for (int r = 0; r < BC_ROWS; ++r) {
         const int64_t i = (int64_t)blockIdx.x * BC_ROWS + r;
         if (i >= P.m) break;
-        for (int c = threadIdx.x; c < S; c += 256) P.bc[i * L + c] = P.B0[i * L + P.rlist[c]];
+        for (int c = threadIdx.x; c < S; c += 256) P.bc[i * ldc + c] = P.B0[i * L + P.rlist[c]];
     }
 }
 hipError_t launch_compact(const Params& P, hipStream_t s) {
@@ -2820,11 +2840,12 @@ __global__ __launch_bounds__(256) void k_se_part(Params P) {
     if (threadIdx.x < SE_RB) sa[threadIdx.x] = threadIdx.x < nr ? al[i0 + threadIdx.x] : 0.0;
     __syncthreads();
     const double* Mw = P.bc ? P.bc : P.B0;
+    const int64_t ldm = P.bc ? (int64_t)P.bc_n[1] : L;  // row pitch (compact: bc_pitch)
     double* out = P.se_part + (int64_t)blockIdx.x * (L + KW + 1);
     for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
         double acc = 0.0;
         if (c < S) {
-            for (int r = 0; r < nr; ++r) acc = fma(Mw[(i0 + r) * L + c], sa[r], acc);
+            for (int r = 0; r < nr; ++r) acc = fma(Mw[(i0 + r) * ldm + c], sa[r], acc);
         } else if (c < S + KW) {
             const int sc = c - S;
             if (sc < tau)

@@ -70,5 +70,7 @@ hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hip
 
 // the grid a persistent launch uses (SPX_LOOP_OVERSUB=1: twice it, for tests)
 int loop_grid_launched(int grid);
+// SPX_LOOP_COOP=1 (diagnostics): hipLaunchCooperativeKernel as in round 1
+bool loop_coop_launch();
 
 }  // namespace spx

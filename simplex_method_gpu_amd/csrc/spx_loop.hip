@@ -441,7 +441,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
             }
             auto compact_row = [&](int64_t i) -> double {
                 double a = (lane == 0 && P.rmap[i] < 0) ? apd[i] : 0.0;
-                const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + i * L2;
+                const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + i * (int64_t)P.bc_n[1]);
                 const int S2 = (Sb + 1) >> 1;
                 for (int k0 = 0; k0 < S2; k0 += 8 * 64) {
                     dbl2 v[8], w[8];
@@ -693,7 +693,16 @@ hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hip
     // loop_prepare) is co-resident without the cooperative launch's check,
     // and the grid barrier is our own (spx_grid.h), so no cooperative queue
     // (MI355X_MICROARCH.md coop-launch: +15-19 us host wall per launch)
+    if (loop_coop_launch())
+        return hipLaunchCooperativeKernel(fn, dim3(c.grid), dim3(c.block), args, (unsigned)c.lds_bytes, s);
     return hipLaunchKernel(fn, dim3(loop_grid_launched(c.grid)), dim3(c.block), args, (size_t)c.lds_bytes, s);
+}
+
+// SPX_LOOP_COOP=1 (diagnostics): the round-1 cooperative launch instead of the
+// plain one (tools/tab_exit_probe.py, the exit-time crash under rocprofv3)
+bool loop_coop_launch() {
+    const char* v = std::getenv("SPX_LOOP_COOP");
+    return v && v[0] == '1';
 }
 
 // SPX_LOOP_OVERSUB=1 (tests): launch 4,096 more workgroups than the
