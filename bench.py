@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--update-rows", type=int, default=0)
     ap.add_argument("--update-block", type=int, default=0)
@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--row-shard", action="store_true",
                     help="N > 1: row-shard an explicit B^-1 over the ranks (SURVEY.md §8f row 1) "
                          "instead of replicating the eta window")
+    ap.add_argument("--persist", choices=["auto", "on", "off"], default="auto",
+                    help="persistent loop kernel (k_loop): the library's choice, forced on, or two-kernel passes")
     ap.add_argument("--no-explicit", action="store_true", help="skip the explicit-B^-1 block")
     ap.add_argument("--no-sharded-pricing", action="store_true",
                     help="skip the C4 column-sharded pricing block (pricing_c4)")
@@ -142,7 +144,8 @@ def main():
                           update_rows=args.update_rows, update_block=args.update_block,
                           price_block=args.price_block, graph_batch=args.graph_batch,
                           row_shard=row_shard and window < 0, window=window,
-                          comm1=(args.comm1 and world == 1))
+                          comm1=(args.comm1 and world == 1),
+                          persist={"auto": None, "on": True, "off": False}[args.persist])
         if multi and (args.minloc == "rccl" or (row_shard and window < 0)):
             obj = [spx.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)

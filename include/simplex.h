@@ -331,8 +331,8 @@ int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
 /* Diagnostic (SPX_FLAG_STAMPS, compact window passes): per workgroup g of the
  * last FTRAN launch (k_ftran_bc), out[4g + k] = s_memrealtime ticks (100 MHz)
- * at k = 0 entry, 1 entering column known, 2 its wave 0's alpha formed,
- * 3 partial published.  Copies min(cap, 4 * grid) values; *count = grid. */
+ * at k = 0 entry, 1 entering column known, 2 A_p on the column list in LDS
+ * (the p-dependent round trip done), 3 partial published.  Copies min(cap, 4 * grid) values; *count = grid. */
 int spx_wg_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
 
 /* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]

@@ -297,8 +297,8 @@ class Context:
 
     def wg_times(self):
         """Per-workgroup clock of the last compact FTRAN launch (stamps=True):
-        array (grid, 4) of 100 MHz ticks at entry, p known, alpha formed,
-        partial published (spx_wg_times)."""
+        array (grid, 4) of 100 MHz ticks at entry, p known, A_p on the list in
+        LDS, partial published (spx_wg_times)."""
         cap = 4 * 8192
         out = np.zeros(cap, dtype=np.uint64)
         cnt = ctypes.c_int64()

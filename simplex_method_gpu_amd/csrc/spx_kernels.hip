@@ -1724,7 +1724,6 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     Sv.nw = st->nw;
     const int Sbc = P.bc_n[0];
     const int64_t ldc = P.bc_n[1];  // compact row pitch (k_bc_list)
-    const unsigned long long t_wg0 = (P.stamps && blockIdx.x == 0) ? rtime() : 0ull;
     const unsigned long long t_wg_entry = P.stamps ? rtime() : 0ull;
     // the compact row's first NCH chunks (S and the state are scalars: one wait)
     const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + ic * ldc);
@@ -1775,10 +1774,10 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
         }
     }
     if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) return;
-    wg0_mark(P, 0, t_wg0);
-    unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
-    stamp_start(slot);
-    wg0_mark(P, 1, t_wg0);
+    // (diagnostics: plain per-workgroup stores only -- the atomic phase
+    // stamps of the other kernels, 512 workgroups on one address, would
+    // themselves delay this kernel's waits)
+    unsigned long long* const slot = nullptr;
     unsigned long long* const wgt = (P.stamps && tid == 0) ? P.stamps + 32 + 4 * (int64_t)blockIdx.x : nullptr;
     if (wgt) {
         wgt[0] = t_wg_entry;
@@ -1816,9 +1815,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     const double aqp = Sv.aq;
     const bool upd_x = Sv.xb_applied < it;
     const double ei = (pend && rowv) ? eta_entry(par ? al1 : al0, i, qp, aqp) : 0.0;
-    unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
-    stamp_stream(win, true);
-    wg0_mark(P, 2, t_wg0);
+    unsigned long long* const win = nullptr;
     // ---- compact FTRAN (as k_update BC): the unit term first (lane 0), then
     // this lane's chunks lane + 64 t ascending, .x before .y; A_p gathered
     // onto the list in LDS blocks of BC_APC columns
@@ -1837,6 +1834,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
         }
         for (int c = cb + (cb == 0 ? BC_RL * BLOCK : 0) + tid; c < ce; c += BLOCK) apc[c - cb] = apd[P.rlist[c]];
         lds_barrier();
+        if (wgt && cb == 0) wgt[2] = rtime();
         const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
         if (rowv) {
             auto take = [&](dbl2 v, int k2) {
@@ -1881,9 +1879,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
         if (lane == 0 && rowv) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
     }
     const double s_x = upd_x ? sxw : 0.0;
-    stamp_stream(win, false);
-    wg0_mark(P, 3, t_wg0);
-    if (wgt) wgt[2] = rtime();
+
     // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partial
     UpdPartial wp = upd_empty();
     if (rowv) {
@@ -1924,7 +1920,6 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             UpdPartial w = red[0];
             for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
             upd_publish_tagged(P, blockIdx.x, w, tag, lane);
-            wg0_mark(P, 4, t_wg0);
             if (wgt) wgt[3] = rtime();
         }
         if (blockIdx.x != gridDim.x - 1) return;

@@ -4,7 +4,7 @@
 # WRITE_SIZE) on an eager C3 workload that covers a fold, and the traffic JSON.
 # usage: tools/gpu_profile.sh rNN
 set -o pipefail
-R=${1:-r02}
+R=${1:-r03}
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/prof_$R"
 mkdir -p "$OUT"

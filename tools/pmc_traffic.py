@@ -12,7 +12,7 @@ import json
 import statistics
 
 
-KERNELS = ("k_price", "k_update", "k_tab_fold", "k_fold")
+KERNELS = ("k_price", "k_ftran_bc", "k_update", "k_tab_fold", "k_fold", "k_bc_gather")
 
 
 def per_kernel(path, counter):
@@ -56,8 +56,10 @@ def main():
                 1024.0 * statistics.median(fv))
     if "k_price" in out:
         out["price_hbm_bytes_per_launch"] = out["k_price"]["hbm_bytes"]
-    if "k_update" in out:
-        out["update_hbm_bytes_per_launch"] = out["k_update"]["hbm_bytes"]
+    upd = "k_ftran_bc" if "k_ftran_bc" in out else "k_update"
+    if upd in out:
+        out["update_kernel"] = upd
+        out["update_hbm_bytes_per_launch"] = out[upd]["hbm_bytes"]
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))

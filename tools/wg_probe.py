@@ -1,6 +1,7 @@
 """Per-workgroup clock of the compact FTRAN pass (k_ftran_bc, stamps=True):
-when each workgroup starts, knows p, has its wave 0's alpha and publishes
-its partial, relative to the earliest start, over several eager passes.
+when each workgroup starts, knows p, has A_p on the column list in LDS and
+publishes its partial, relative to the earliest start, over several eager
+passes.
     python tools/wg_probe.py [--m 4096 --n 16384 --passes 6]"""
 import argparse
 import json
@@ -27,7 +28,7 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, graph_batch=-1) as
         t = (t - t[:, 0].min()) * 0.01  # us
         rows.append(t)
 T = np.stack(rows)  # passes x grid x 4
-names = ["entry", "p_known", "alpha", "publish"]
+names = ["entry", "p_known", "ap_in_lds", "publish"]
 out = {}
 for k, nm in enumerate(names):
     v = T[:, :, k]
@@ -37,7 +38,7 @@ late = T[:, :, 3].mean(axis=0)
 order = np.argsort(-late)[:12]
 out["slowest_wg"] = [{"wg": int(g), "xcd": int(g % 8), "publish_us": round(float(late[g]), 2),
                       "entry_us": round(float(T[:, g, 0].mean()), 2), "p_us": round(float(T[:, g, 1].mean()), 2),
-                      "alpha_us": round(float(T[:, g, 2].mean()), 2)} for g in order]
+                      "ap_lds_us": round(float(T[:, g, 2].mean()), 2)} for g in order]
 xcd = [round(float(late[np.arange(len(late)) % 8 == x].mean()), 2) for x in range(8)]
 out["publish_mean_by_xcd"] = xcd
 half = len(late) // 2
