@@ -332,7 +332,10 @@ int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 /* Diagnostic (SPX_FLAG_STAMPS, compact window passes): per workgroup g of the
  * last FTRAN launch (k_ftran_bc), out[4g + k] = s_memrealtime ticks (100 MHz)
  * at k = 0 entry, 1 entering column known, 2 A_p on the column list in LDS
- * (the p-dependent round trip done), 3 partial published.  Copies min(cap, 4 * grid) values; *count = grid. */
+ * (the p-dependent round trip done), 3 partial published; then, per
+ * workgroup h of the last pricing launch (k_price), out[4 grid + 2h + k] at
+ * k = 0 start, 1 end of its column loop.  Copies min(cap, 4 grid + 2 price
+ * grid) values; *count = grid. */
 int spx_wg_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
 
 /* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]

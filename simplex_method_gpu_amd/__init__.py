@@ -299,11 +299,21 @@ class Context:
         """Per-workgroup clock of the last compact FTRAN launch (stamps=True):
         array (grid, 4) of 100 MHz ticks at entry, p known, A_p on the list in
         LDS, partial published (spx_wg_times)."""
-        cap = 4 * 8192
+        cap = 4 * 4096 + 2 * 4096
         out = np.zeros(cap, dtype=np.uint64)
         cnt = ctypes.c_int64()
         check(self._L.spx_wg_times(self._h, _ptr(out), cap, ctypes.byref(cnt)))
         return out[: 4 * cnt.value].reshape(cnt.value, 4)
+
+    def price_wg_times(self):
+        """Per-workgroup (start, end of the column loop) of the last pricing
+        launch (stamps=True), 100 MHz ticks (spx_wg_times)."""
+        cap = 4 * 4096 + 2 * 4096
+        out = np.zeros(cap, dtype=np.uint64)
+        cnt = ctypes.c_int64()
+        check(self._L.spx_wg_times(self._h, _ptr(out), cap, ctypes.byref(cnt)))
+        g = self.config()["price_grid"]
+        return out[4 * cnt.value: 4 * cnt.value + 2 * g].reshape(g, 2)
 
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""

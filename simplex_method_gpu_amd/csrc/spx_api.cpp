@@ -395,7 +395,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (x->opts.price_block == 256 || x->opts.price_block == 512 || x->opts.price_block == 1024)
         pc.block = x->opts.price_block;
     else
-        pc.block = ybytes <= 72 * 1024 ? 512 : 1024;
+        // 8 waves per CU either way: with y (and the base row) taking most of
+        // LDS there is one workgroup per CU, and a 1024-thread workgroup would
+        // cap k_price at 128 VGPRs and spill (C5: 1,158 vs 977 us per pass)
+        pc.block = 512;
     const size_t red_bytes = (size_t)(pc.block / 64) * sizeof(PricePartial) + 16;
     const size_t lds_cap = 150 * 1024;
     pc.lds_y = ybytes + red_bytes <= lds_cap && !(x->opts.flags & SPX_FLAG_GLOBAL_Y) && !P.tab;
@@ -466,13 +469,14 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         x->lcfg.block = x->opts.loop_block;
         HIP_TRY(loop_prepare(P, x->cus, x->lcfg, bc_possible(x, P)));
         P.bc_lds = x->lcfg.bc_lds;
-        // measured (tools/loop_sweep.sh): the persistent loop wins once the
-        // base row is read from L2 (C5: 729 vs 681 it/s) and loses at C3
-        // (8.3k vs 9.3k it/s), so by default only then
-        // (the compact FTRAN operand does not change this: at C5 its two-kernel
-        // pass ran 700 it/s, pricing with the base row from L2 1,384 us, against
-        // the dense persistent loop's 740; tools/r02_c5compact.sh)
-        const bool want = (x->opts.flags & SPX_FLAG_PERSIST) || !x->lcfg.lds_r;
+        // opt-in only (SPX_FLAG_PERSIST).  Rounds 1-2 ran it by default where y_w
+        // and the base row do not both fit in LDS (C5), because the two-kernel
+        // pass's pricing, then a 1024-thread workgroup capped at 128 VGPRs,
+        // spilled: C5 690 vs 959 it/s.  With 512-thread pricing workgroups the
+        // two-kernel pass runs C5 at 957 it/s (profiles/r03_bench_c5*.json),
+        // so one dispatch -- two kernels per pass -- holds at every size and
+        // every rank count (k_loop is single-rank)
+        const bool want = (x->opts.flags & SPX_FLAG_PERSIST) != 0;
         if (x->lcfg.ok && want) {
             SPX_TRY(x->alloc(&x->la.pp, (size_t)x->lcfg.grid));
             SPX_TRY(x->alloc(&x->la.up, (size_t)x->lcfg.grid));
@@ -508,7 +512,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // upload), while A_p's gather fits beside the k_update LDS
     x->bc_want = bc_possible(x, P) && (!x->persist || x->lcfg.bc_lds > 0);
     if (x->opts.flags & SPX_FLAG_STAMPS) {
-        SPX_TRY(x->alloc(&P.stamps, (size_t)(32 + 4 * std::max<int64_t>(uc.grid, 1))));
+        // 32 phase slots, 4 per k_ftran_bc workgroup (up to 4096), 2 per k_price workgroup
+        SPX_TRY(x->alloc(&P.stamps, (size_t)(32 + 4 * 4096 + 2 * 4096)));
         SPX_TRY(reset_stamps(x));
     }
     SPX_TRY(x->alloc(&x->send, (size_t)P.pr_stride));
@@ -1406,8 +1411,13 @@ int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
     if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
     if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
     HIP_TRY(hipStreamSynchronize(x->stream));
-    const int64_t k = std::min<int64_t>(cap, 4 * (int64_t)x->ucfg.grid);
-    if (k > 0) HIP_TRY(hipMemcpy(out, x->P.stamps + 32, sizeof(uint64_t) * (size_t)k, hipMemcpyDeviceToHost));
+    // k_ftran_bc: 4 per workgroup; then k_price: 2 per workgroup (start, end)
+    const int64_t nu = 4 * (int64_t)std::min(x->ucfg.grid, 4096), np = 2 * (int64_t)std::min(x->pcfg.grid, 4096);
+    std::vector<uint64_t> h((size_t)(4 * 4096 + np));
+    HIP_TRY(hipMemcpy(h.data(), x->P.stamps + 32, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
+    int64_t k = 0;
+    for (int64_t i = 0; i < nu && k < cap; ++i) out[k++] = h[(size_t)i];
+    for (int64_t i = 0; i < np && k < cap; ++i) out[k++] = h[(size_t)(4 * 4096 + i)];
     if (count) *count = x->ucfg.grid;
     return SPX_OK;
 }

@@ -145,6 +145,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // speculative: this wave's first non-basic column, loaded together with the
     // status word (index clamped into the list; validated against nb_count)
     const int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
+    const unsigned long long t_pw0 = P.stamps ? rtime() : 0ull;
     const DevState S = st_snapshot(st);
     if (stopped(S)) return;
     unsigned long long* const slot = P.stamps;
@@ -587,6 +588,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
     if (lane == 0) red[wave] = PricePartial{best, bj, bw, be};
     __syncthreads();
+    if (P.stamps && tid == 0 && blockIdx.x < 4096) {  // diagnostics: this workgroup's start and end
+        unsigned long long* pw = P.stamps + 32 + 4 * 4096 + 2 * (int64_t)blockIdx.x;
+        pw[0] = t_pw0;
+        pw[1] = rtime();
+    }
     if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
         if (tid == 0) {
             PricePartial w = red[0];

@@ -13,8 +13,9 @@ its third window on the folded state:
   - C4 default: two-kernel window passes with the compact FTRAN operand;
   - C4 as an in-process group of 8 column shards (B^-1 replicated, MINLOC
     merge; the north-star partitioning, SURVEY.md §8e);
-  - C5 default: the persistent loop k_loop (compact FTRAN, A_p gathered on the
-    column list into LDS); C5 with two-kernel passes; C5 as a 2-shard group.
+  - C5 default: two-kernel passes (compact FTRAN, the base row read from L2);
+    C5 on the persistent loop k_loop (opt-in; A_p gathered on the column list
+    into LDS); C5 as a 2-shard group (the default dispatch, two ranks).
 Tolerances (fp64): (p, q) identical for every pivot; the same
 basis order; x_b and y within 1e-9 (relative max-norm); z within 1e-9.
 """
@@ -104,12 +105,12 @@ def test_c4_group8_matches_oracle(spx, c4):
     _group(spx, c4, 8)
 
 
-def test_c5_default_persistent_matches_oracle(spx, c5):
-    _single(spx, c5, expect_persistent=True)
+def test_c5_default_matches_oracle(spx, c5):
+    _single(spx, c5, expect_persistent=False)
 
 
-def test_c5_two_kernel_matches_oracle(spx, c5):
-    _single(spx, c5, expect_persistent=False, persist=False)
+def test_c5_persistent_matches_oracle(spx, c5):
+    _single(spx, c5, expect_persistent=True, persist=True)
 
 
 def test_c5_group2_matches_oracle(spx, c5):

@@ -89,17 +89,18 @@ def test_loop_refactor_and_timing(spx, oracle):
     assert lt["clock_passes"] > 0 and lt["price_us"] > 0 and lt["ftran_us"] > 0
 
 
-def test_loop_auto_on_large_m(spx):
-    """By default the persistent loop runs only where it measured faster: when
-    y_w and the pending base row do not both fit in LDS (m > ~9400).  Both
-    forms read only B_w's non-unit columns (the compact operand: none yet at
-    the slack basis)."""
+def test_loop_opt_in_only(spx):
+    """Two-kernel passes are the default at every size, so a single GPU runs
+    the dispatch that N ranks run (the persistent loop is single-rank); the
+    loop is opt-in.  Both forms read only B_w's non-unit columns (the compact
+    operand: none yet at the slack basis)."""
     with spx.Context(m=1000, n=3000, seed=0, window=64) as ctx:
         assert ctx.config()["persistent"] == 0 and ctx.ftran_cols() == 0
     with spx.Context(m=12000, n=13000, seed=0, window=64) as ctx:
-        assert ctx.config()["persistent"] == 1 and ctx.ftran_cols() == 0
-    with spx.Context(m=12000, n=13000, seed=0, window=64, persist=False) as ctx:
         assert ctx.config()["persistent"] == 0 and ctx.ftran_cols() == 0
+        assert ctx.config()["price_block"] == 512
+    with spx.Context(m=12000, n=13000, seed=0, window=64, persist=True) as ctx:
+        assert ctx.config()["persistent"] == 1 and ctx.ftran_cols() == 0
 
 
 @pytest.mark.parametrize("tableau", [False, True], ids=["k_loop", "k_tab_loop"])

@@ -19,7 +19,7 @@ ap.add_argument("--n", type=int, default=16384)
 ap.add_argument("--passes", type=int, default=6)
 ap.add_argument("--warm", type=int, default=70)
 a = ap.parse_args()
-rows = []
+rows, prow = [], []
 with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, graph_batch=-1) as ctx:
     ctx.iterate(a.warm)
     for _ in range(a.passes):
@@ -27,6 +27,8 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, graph_batch=-1) as
         t = ctx.wg_times().astype(np.int64)
         t = (t - t[:, 0].min()) * 0.01  # us
         rows.append(t)
+        pt = ctx.price_wg_times().astype(np.int64)
+        prow.append((pt - pt[:, 0].min()) * 0.01)
 T = np.stack(rows)  # passes x grid x 4
 names = ["entry", "p_known", "ap_in_lds", "publish"]
 out = {}
@@ -43,4 +45,11 @@ xcd = [round(float(late[np.arange(len(late)) % 8 == x].mean()), 2) for x in rang
 out["publish_mean_by_xcd"] = xcd
 half = len(late) // 2
 out["publish_mean_first_half_vs_second"] = [round(float(late[:half].mean()), 2), round(float(late[half:].mean()), 2)]
+PT = np.stack(prow)  # passes x price grid x 2
+pe = PT[:, :, 1]
+out["price_wg_end"] = {"p10": round(float(np.percentile(pe, 10)), 2), "p50": round(float(np.median(pe)), 2),
+                       "p90": round(float(np.percentile(pe, 90)), 2), "max": round(float(pe.max()), 2),
+                       "start_max": round(float(PT[:, :, 0].max()), 2)}
+out["price_wg_end_by_xcd"] = [round(float(pe.mean(axis=0)[np.arange(pe.shape[1]) % 8 == x].mean()), 2)
+                              for x in range(8)]
 print(json.dumps(out, indent=1))
