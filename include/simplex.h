@@ -329,13 +329,18 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
 #define SPX_PHASES 18
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
-/* Diagnostic (SPX_FLAG_STAMPS, compact window passes): per workgroup g of the
- * last FTRAN launch (k_ftran_bc), out[4g + k] = s_memrealtime ticks (100 MHz)
- * at k = 0 entry, 1 entering column known, 2 A_p on the column list in LDS
- * (the p-dependent round trip done), 3 partial published; then, per
- * workgroup h of the last pricing launch (k_price), out[4 grid + 2h + k] at
- * k = 0 start, 1 end of its column loop.  Copies min(cap, 4 grid + 2 price
- * grid) values; *count = grid. */
+/* Diagnostic (SPX_FLAG_STAMPS, compact window passes): the clocks of the
+ * last two passes, s_memrealtime ticks (100 MHz), one block per pass parity
+ * (iteration & 1, parity 0 first).  A block holds, per workgroup g of that
+ * pass's FTRAN launch (k_ftran_bc), 4 ticks at k = 0 entry, 1 entering column
+ * known, 2 A_p on the column list in LDS (the p-dependent round trip done),
+ * 3 partial published (4 grid values); then per workgroup h of its pricing
+ * launch (k_price) 4 ticks: start, end of its column loop, the deferred
+ * ratio-test tail reduced, the staging in LDS (4 price grid values); then
+ * the tick at which the FTRAN tail had issued the pivot's
+ * bookkeeping (1 value), then the tick at which the diagnostic one-wave
+ * kernel launched before the FTRAN pass started (SPX_DIAG_MARK=1; 1 value).
+ * Copies min(cap, 2 (4 grid + 4 price grid + 2)) values; *count = grid. */
 int spx_wg_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
 
 /* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]
@@ -362,8 +367,11 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * threads per workgroup, [5] update rows per wave, [6] update workgroups,
  * [7] passes per captured hipGraph (0 = eager), [8] persistent loop kernel
  * in use (1) or not (0), [9] its threads per workgroup, [10] window tableau
- * (SPX_FLAG_TABLEAU) in use, [11] workgroups of the persistent loop kernel. */
-#define SPX_CONFIG_FIELDS 12
+ * (SPX_FLAG_TABLEAU) in use, [11] workgroups of the persistent loop kernel,
+ * [12] the ratio-test tail deferred into the next pricing pass (1; compact
+ * window passes on one rank, SPX_DEFER_TAIL=0 turns it off) or run by the
+ * FTRAN pass's last workgroup (0). */
+#define SPX_CONFIG_FIELDS 13
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Columns of B^-1 the FTRAN stream reads per row: m, or with the eta window's

@@ -296,24 +296,26 @@ class Context:
                 "update_ms": tu.value, "update_launches": nu.value}
 
     def wg_times(self):
-        """Per-workgroup clock of the last compact FTRAN launch (stamps=True):
-        array (grid, 4) of 100 MHz ticks at entry, p known, A_p on the list in
-        LDS, partial published (spx_wg_times)."""
-        cap = 4 * 4096 + 2 * 4096
-        out = np.zeros(cap, dtype=np.uint64)
+        """Per-pass clocks of the last two compact window passes (stamps=True,
+        spx_wg_times), 100 MHz ticks, indexed by pass parity (iteration & 1):
+        a list of two dicts {"ftran": (grid, 4) entry / p known / A_p on the
+        list in LDS / partial published, "price": (price grid, 4) start / end
+        of the column loop / deferred tail reduced / staging in LDS, "tail": the tick the FTRAN tail had issued the
+        bookkeeping, "mark": the start of the SPX_DIAG_MARK=1 probe kernel
+        launched before the FTRAN pass (0 without it)}."""
+        cfg = self.config()
+        g, gp = cfg["update_grid"], cfg["price_grid"]
+        per = 4 * min(g, 4096) + 4 * min(gp, 4096) + 2
+        out = np.zeros(2 * per, dtype=np.uint64)
         cnt = ctypes.c_int64()
-        check(self._L.spx_wg_times(self._h, _ptr(out), cap, ctypes.byref(cnt)))
-        return out[: 4 * cnt.value].reshape(cnt.value, 4)
-
-    def price_wg_times(self):
-        """Per-workgroup (start, end of the column loop) of the last pricing
-        launch (stamps=True), 100 MHz ticks (spx_wg_times)."""
-        cap = 4 * 4096 + 2 * 4096
-        out = np.zeros(cap, dtype=np.uint64)
-        cnt = ctypes.c_int64()
-        check(self._L.spx_wg_times(self._h, _ptr(out), cap, ctypes.byref(cnt)))
-        g = self.config()["price_grid"]
-        return out[4 * cnt.value: 4 * cnt.value + 2 * g].reshape(g, 2)
+        check(self._L.spx_wg_times(self._h, _ptr(out), out.size, ctypes.byref(cnt)))
+        res = []
+        for par in range(2):
+            b = out[par * per: (par + 1) * per]
+            nu, npr = 4 * min(g, 4096), 4 * min(gp, 4096)
+            res.append({"ftran": b[:nu].reshape(-1, 4), "price": b[nu: nu + npr].reshape(-1, 4),
+                        "tail": int(b[nu + npr]), "mark": int(b[nu + npr + 1])})
+        return res
 
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""
@@ -369,10 +371,10 @@ class Context:
 
     def config(self):
         """Resolved representation and launch geometry (spx_config)."""
-        out = (ctypes.c_int32 * 12)()
+        out = (ctypes.c_int32 * 13)()
         check(self._L.spx_config(self._h, out))
         keys = ("window", "price_block", "price_grid", "price_lds", "update_block", "update_rows", "update_grid",
-                "graph_batch", "persistent", "loop_block", "tableau", "loop_grid")
+                "graph_batch", "persistent", "loop_block", "tableau", "loop_grid", "defer_tail")
         return dict(zip(keys, list(out)))
 
 

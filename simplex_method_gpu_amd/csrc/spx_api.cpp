@@ -114,6 +114,7 @@ struct spx_ctx {
     bool bc_want = false;      // compact FTRAN operand wanted (allocated by set_slack_flags)
     bool slack_ident = false;  // A[:, n-m:] = I (checked before setup_common)
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
+    bool defer_tail = false;      // loop passes defer the ratio-test tail into k_price (Params::defer_tail)
 
     // graph replay of `batch` passes
     hipGraphExec_t graph_exec = nullptr;
@@ -446,6 +447,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     uc.block = ub;
     uc.rows = rows;
     uc.bc_entry = !env_off("SPX_FTRAN_BC_ENTRY");
+    uc.mark = env_on("SPX_DIAG_MARK");
     const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
     uc.grid = (int)std::max<int64_t>(1, (P.mloc + rows_per_wg - 1) / rows_per_wg);
     if (P.tab) {  // k_tab_update: one lane per row, 256 rows per workgroup
@@ -513,7 +515,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     x->bc_want = bc_possible(x, P) && (!x->persist || x->lcfg.bc_lds > 0);
     if (x->opts.flags & SPX_FLAG_STAMPS) {
         // 32 phase slots, 4 per k_ftran_bc workgroup (up to 4096), 2 per k_price workgroup
-        SPX_TRY(x->alloc(&P.stamps, (size_t)(32 + 4 * 4096 + 2 * 4096)));
+        SPX_TRY(x->alloc(&P.stamps, (size_t)STAMP_WORDS));
         SPX_TRY(reset_stamps(x));
     }
     SPX_TRY(x->alloc(&x->send, (size_t)P.pr_stride));
@@ -535,7 +537,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // us; C3 explicit 126.5 -> 128.5 us (its stream waits for the reduction),
     // so not for large explicit passes
     x->defer_ok = (P.win || m <= 2048) && !x->use_comm && !P.split_tail && !P.row_shard &&
-                  !(x->opts.flags & (SPX_FLAG_STAMPS | SPX_FLAG_PRICE_TAIL));
+                  !(x->opts.flags & SPX_FLAG_PRICE_TAIL);
     P.price_out = x->send;
     P.price_in = x->use_comm ? x->recv : x->send;
     P.nin = G;
@@ -648,6 +650,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     if (fold) {
         hipEvent_t f0 = nullptr, f1 = nullptr;
         if (timed) SPX_TRY(fold_events(x, &f0, &f1));
+        if (x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));  // the fold reads the pivot's state
         if (f0) HIP_TRY(hipEventRecord(f0, x->stream));
         HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
         if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
@@ -656,6 +659,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     HIP_TRY(launch_se_prep(x->P, x->stream));  // steepest edge: after the fold, before pricing
     Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
     Pp.defer_price = x->defer_ok ? 1 : 0;
+    Pp.defer_tail = x->defer_tail ? 1 : 0;
     HIP_TRY(launch_price(Pp, x->pcfg, x->stream, p0, p1));
     if (x->use_comm) {
         if (x->mbox_ready) {
@@ -886,6 +890,7 @@ int iterate_raw(spx_ctx* x, int64_t k) {
         }
     }
     for (int64_t i = 0; i < left; ++i) SPX_TRY(enqueue_pass(x, x->timing));
+    if (x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));  // the last pass's tail, before any readback
     return read_state(x);
 }
 
@@ -1037,6 +1042,20 @@ int set_slack_flags(spx_ctx* x) {
         SPX_TRY(x->alloc(&P.rmap, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rleft, (size_t)x->L));
         SPX_TRY(x->alloc(&P.bc_n, 4));
+    }
+    // deferred ratio-test tail (TailRec, spx_device.h): compact FTRAN passes
+    // (k_ftran_bc, one row per wave) with 512-thread pricing -- the reduction
+    // shape k_price, k_apply_tail and the FTRAN tail share -- on one rank, the
+    // pricing tail deferred as well.  Measured at C3 (tools/fuse_est.py, the
+    // timing-only estimate): 79.8 -> 73.9 us per pass.  SPX_DEFER_TAIL=0 keeps
+    // the tail in the FTRAN pass.
+    const UpdateCfg& uc = x->ucfg;
+    if (x->P.bc && x->defer_ok && !x->persist && !x->P.steep && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
+        uc.block == 512 && x->pcfg.block == 512 && !env_off("SPX_DEFER_TAIL")) {
+        SPX_TRY(x->alloc(&x->P.trec, 1));
+        HIP_TRY(hipMemset(x->P.trec, 0, sizeof(TailRec)));
+        x->P.tail_parts = uc.grid;
+        x->defer_tail = true;
     }
     return SPX_OK;
 }
@@ -1411,13 +1430,17 @@ int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
     if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
     if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
     HIP_TRY(hipStreamSynchronize(x->stream));
-    // k_ftran_bc: 4 per workgroup; then k_price: 2 per workgroup (start, end)
-    const int64_t nu = 4 * (int64_t)std::min(x->ucfg.grid, 4096), np = 2 * (int64_t)std::min(x->pcfg.grid, 4096);
-    std::vector<uint64_t> h((size_t)(4 * 4096 + np));
-    HIP_TRY(hipMemcpy(h.data(), x->P.stamps + 32, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
+    // per parity: k_ftran_bc 4 per workgroup, k_price 4 per workgroup, the tail end, k_mark
+    const int64_t gu = std::min(x->ucfg.grid, 4096), gp = std::min(x->pcfg.grid, 4096);
+    std::vector<uint64_t> h((size_t)STAMP_WORDS);
+    HIP_TRY(hipMemcpy(h.data(), x->P.stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
     int64_t k = 0;
-    for (int64_t i = 0; i < nu && k < cap; ++i) out[k++] = h[(size_t)i];
-    for (int64_t i = 0; i < np && k < cap; ++i) out[k++] = h[(size_t)(4 * 4096 + i)];
+    for (int par = 0; par < 2; ++par) {
+        for (int64_t i = 0; i < 4 * gu && k < cap; ++i) out[k++] = h[(size_t)(STAMP_FTRAN + par * 4 * 4096 + i)];
+        for (int64_t i = 0; i < 4 * gp && k < cap; ++i) out[k++] = h[(size_t)(STAMP_PRICE + par * 4 * 4096 + i)];
+        if (k < cap) out[k++] = h[(size_t)(STAMP_TAIL + par)];
+        if (k < cap) out[k++] = h[(size_t)(STAMP_TAIL + 2 + par)];
+    }
     if (count) *count = x->ucfg.grid;
     return SPX_OK;
 }
@@ -1708,6 +1731,7 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[9] = x->persist ? x->lcfg.block : 0;
     out[10] = x->P.tab;
     out[11] = x->persist ? x->lcfg.grid : 0;
+    out[12] = x->defer_tail ? 1 : 0;
     return SPX_OK;
 }
 

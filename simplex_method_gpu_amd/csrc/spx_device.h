@@ -118,6 +118,27 @@ constexpr int UPD_WORDS = 14;
 // tagged pricing partial (k_price's own tail): 4 eight-byte fields as 8 words
 constexpr int PRICE_WORDS = 8;
 
+// Deferred ratio-test tail (Params::defer_tail): the compact FTRAN pass
+// publishes its workgroup partials and this record and ends; the next
+// pricing pass reduces the partials in every workgroup (the leaving row q
+// its base row needs) and its workgroup 0 applies the bookkeeping; a
+// one-workgroup k_apply_tail does it before a fold and at the end of a
+// batch.  fresh = 1 from the FTRAN pass that wrote it until k_apply_tail, or
+// an FTRAN pass that stops, clears it.
+struct alignas(16) TailRec {
+    int64_t it;      // iteration of the pivot
+    int64_t p;       // entering column
+    double e_rep;    // the reduced cost the bookkeeping records (Devex: its key's e)
+    double c_p;      // c[p]
+    double wp;       // Devex: W[p]
+    int32_t cnt;     // nb_count before the pivot
+    int32_t kp;      // nb_pos[p] (-1: not on this rank's list)
+    int32_t last;    // nb_list[cnt - 1]
+    int32_t nw;      // window count before the pivot
+    int32_t fresh;
+    int32_t pad[3];
+};
+
 struct alignas(16) DevState {
     int32_t status;      // ST_*
     int32_t nb_count;    // entries in nb_list
@@ -145,6 +166,14 @@ struct alignas(16) DevState {
 __host__ __device__ inline bool argmin_better(double v, int64_t j, double bv, int64_t bj) {
     return (v < bv) || (v == bv && j < bj);
 }
+
+// SPX_FLAG_STAMPS layout past the 32 phase words, by pass parity (it & 1):
+// k_ftran_bc 4 ticks per workgroup, k_price 4 per workgroup, and the compact
+// FTRAN tail's end
+constexpr int64_t STAMP_FTRAN = 32;
+constexpr int64_t STAMP_PRICE = STAMP_FTRAN + 2 * 4 * 4096;
+constexpr int64_t STAMP_TAIL = STAMP_PRICE + 2 * 4 * 4096;
+constexpr int64_t STAMP_WORDS = STAMP_TAIL + 8;
 
 struct Params {
     // problem
@@ -197,7 +226,8 @@ struct Params {
     const unsigned char* rs_recv;  // nin entries of rs_stride bytes
     int64_t rs_stride;
     // diagnostics (SPX_FLAG_STAMPS): per kernel {min WG start, sum body, sum tail}
-    // in s_memrealtime ticks (100 MHz); nullptr in normal runs
+    // in s_memrealtime ticks (100 MHz) in the first 32 words, then per-pass
+    // clocks double-buffered by the pass parity (STAMP_*); nullptr in normal runs
     unsigned long long* stamps;
     // eta window (see above); win = KW, 0 = explicit B^-1 updated every pivot
     int32_t win;
@@ -233,6 +263,11 @@ struct Params {
     // price_grid partials itself (no last-workgroup fan-in, no ticket)
     int32_t defer_price;
     int32_t price_grid;
+    // deferred ratio-test tail (TailRec above; one rank, compact window
+    // passes): tail_parts = the FTRAN pass's workgroups
+    int32_t defer_tail;
+    int32_t tail_parts;
+    TailRec* trec;
     // window tableau (SPX_FLAG_TABLEAU): T_w = B_w A (L x n,
     // column-major like A) and dw = y_w A - c (n), both folded with B_w, so a
     // pass reads T_w[q_tau, j], dw[j] and Wt[j][.] per column instead of A_j,

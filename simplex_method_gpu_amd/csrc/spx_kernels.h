@@ -20,12 +20,15 @@ struct UpdateCfg {
     int rows;   // B^-1 rows per wave (1/2/4/8)
     int grid;   // ceil(m / (block / 64 * rows))
     int bc_entry;  // compact FTRAN, 1 row per wave: k_ftran_bc (1) or k_update<..., BC> (0)
+    int mark;      // diagnostic: k_mark before the launch (SPX_DIAG_MARK=1, stamps only)
 };
 
 bool kernels_inplace();  // B^-1 updated in place (one buffer) or ping-pong
 hipError_t price_prepare(const PriceCfg& c, int* blocks_per_cu);
 hipError_t launch_price(const Params& P, const PriceCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// a pending deferred ratio-test tail (Params::defer_tail), applied on its own
+hipError_t launch_apply_tail(const Params& P, hipStream_t s);
 hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n, int64_t L, uint64_t seed,
                            hipStream_t s);
 hipError_t launch_reset(const Params& P, hipStream_t s);

@@ -121,6 +121,28 @@ __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, 
 // Pieces of the deferred pivot (one definition, so every consumer — k_price,
 // k_update, k_flush, k_materialize — produces the same bits)
 // ---------------------------------------------------------------------------
+// The workgroup's best wave partial, chosen on (val, idx) scalars and read
+// back from LDS by index: selecting whole PricePartial structs in a loop put
+// the running winner in scratch, and a kernel with a private segment paid
+// about 4 us more at its kernel boundary
+template <int WAVES>
+__device__ __forceinline__ int best_wave(const PricePartial* red) {
+    double bv = red[0].val;
+    int64_t bi = red[0].idx;
+    int bk = 0;
+#pragma unroll
+    for (int i = 1; i < WAVES; ++i) {
+        const double v = red[i].val;
+        const int64_t x = red[i].idx;
+        if (argmin_better(v, x, bv, bi)) {
+            bv = v;
+            bi = x;
+            bk = i;
+        }
+    }
+    return bk;
+}
+
 // ---------------------------------------------------------------------------
 // Pricing + entering argmin
 // ---------------------------------------------------------------------------
@@ -130,6 +152,12 @@ __device__ __forceinline__ unsigned long long tail_mark(const Params& P, int k, 
 // stream, each column reads T_w[q_tau, j], dw[j] and its Wt row; 4 / 5 = 1 / 2
 // with steepest-edge pricing (P.steep): a third dot v.A_j per column, v =
 // B_w^T alpha (P.se_v) in LDS beside y and the base row (4) or from global (5).
+template <int BLOCK, bool PLAIN = false>
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag = 0,
+                                             bool* timed_out = nullptr);
+// the deferred ratio-test tail's bookkeeping (TailRec; defined with the tail)
+__device__ __forceinline__ void apply_deferred_tail(const Params& P, DevState* st, const TailRec& R,
+                                                    const UpdPartial& t);
 template <int BLOCK, bool LDS_Y, int WM>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
@@ -144,12 +172,95 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int idx0 = blockIdx.x * WAVES + wave;
     // speculative: this wave's first non-basic column, loaded together with the
     // status word (index clamped into the list; validated against nb_count)
-    const int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
+    int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
     const unsigned long long t_pw0 = P.stamps ? rtime() : 0ull;
     const DevState S = st_snapshot(st);
-    if (stopped(S)) return;
+    // the fields the pass prices with (fresh: derived from the deferred tail;
+    // kept as scalars -- assigning into the snapshot put it in scratch)
+    int64_t s_iter = S.iter, s_q = S.q, s_leave = S.leave;
+    double s_aq = S.aq, s_sy = S.s_y, s_wp = S.wp;
+    int32_t s_nb = S.nb_count, s_nw = S.nw;
+    // Deferred ratio-test tail (TailRec, P.defer_tail): the previous FTRAN
+    // pass left its workgroup partials and this record.  Every workgroup
+    // reduces the partials itself (the same reduction as the FTRAN tail, so
+    // the same bits) and prices with the state the bookkeeping produces;
+    // workgroup 0 applies that bookkeeping meanwhile.  No workgroup reads a
+    // state word workgroup 0 writes: the list is read through the two slots
+    // the pivot changes (nbl), SY[tau] is the derived s_y.
+    bool fresh = false;
+    int32_t pk_a = -1, pk_b = -1;
+    int64_t pv_a = 0, pv_b = 0;
+    // the bookkeeping's inputs for workgroup 0's thread 0, which applies them
+    // after its columns (issued first, its stores would hold up the waits for
+    // its own staging loads: vmcnt retires in order)
+    __shared__ TailRec s_rec;
+    __shared__ UpdPartial s_tp;
+    if (P.defer_tail) {
+        const TailRec R = *P.trec;
+        fresh = R.fresh != 0;
+        if (fresh) {
+            __shared__ UpdPartial s_ured[WAVES];
+            const UpdPartial t = reduce_update_partials<BLOCK, true>(P, s_ured, P.tail_parts);
+            const int64_t q = t.idx;
+            const bool unb = t.nonpos == P.m || q < 0 || q >= P.m;
+            if (blockIdx.x == 0 && tid == 0) {
+                if (unb) apply_deferred_tail(P, st, R, t);
+                s_rec.it = R.it;  // (field by field: a struct copy went through scratch)
+                s_rec.p = R.p;
+                s_rec.e_rep = R.e_rep;
+                s_rec.c_p = R.c_p;
+                s_rec.wp = R.wp;
+                s_rec.cnt = R.cnt;
+                s_rec.kp = R.kp;
+                s_rec.last = R.last;
+                s_rec.nw = R.nw;
+                s_tp.idx = t.idx;
+                s_tp.nonpos = t.nonpos;
+                s_tp.T = t.T;
+                s_tp.a_w = t.a_w;
+                s_tp.cb_w = t.cb_w;
+                s_tp.bix_w = t.bix_w;
+            }
+            if (unb) return;  // Unbounded (v4:319-322; workgroup 0 has recorded it)
+            s_iter = R.it + 1;
+            s_q = q;
+            s_aq = t.a_w;
+            s_sy = y_scalar(t.T, t.a_w, t.cb_w, R.c_p);
+            s_nw = R.nw + 1;
+            if (P.devex) {
+                s_leave = t.bix_w;
+                s_wp = R.wp;
+            }
+            // pivot_bookkeeping's list edit: p's slot takes the last entry,
+            // the leaving column joins at the end
+            int32_t c1 = R.cnt;
+            if (R.kp >= 0) {
+                --c1;
+                if (R.kp != c1) {
+                    pk_b = R.kp;
+                    pv_b = R.last;
+                }
+            }
+            if (owns_col(P, t.bix_w)) {
+                pk_a = c1;
+                pv_a = t.bix_w;
+                ++c1;
+            }
+            s_nb = c1;
+            if (idx0 == pk_a) j0 = pv_a;
+            else if (idx0 == pk_b) j0 = pv_b;
+        }
+    }
+    const unsigned long long t_pw1 = P.stamps ? rtime() : 0ull;  // the deferred tail is reduced
+    auto nbl = [&](int idx) -> int64_t {
+        return idx == pk_a ? pv_a : (idx == pk_b ? pv_b : (int64_t)P.nb_list[idx]);
+    };
+    if (S.status != ST_RUNNING || s_iter >= S.limit) {
+        if (fresh && blockIdx.x == 0 && tid == 0) apply_deferred_tail(P, st, s_rec, s_tp);
+        return;
+    }
     unsigned long long* const slot = P.stamps;
-    stamp_start(slot);
+    if (!P.defer_price) stamp_start(slot);  // (deferred passes: per-workgroup clocks only, below)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int64_t L = P.L;
     const int64_t L2 = L >> 1;
@@ -159,9 +270,9 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     PricePartial* red = reinterpret_cast<PricePartial*>(smem + (LDS_Y ? L * 8 : 0) + (LDS_R ? L * 8 : 0) +
                                                         (LDS_V ? L * 8 : 0));
     int* s_last = reinterpret_cast<int*>(red + WAVES);
-    const int nb = S.nb_count;
+    const int nb = s_nb;
 
-    const int64_t it = S.iter;
+    const int64_t it = s_iter;
     const bool wg0 = blockIdx.x == 0;
     constexpr int YB = 4;
     const dbl2* yin = reinterpret_cast<const dbl2*>(S.y_buf ? P.y1 : P.y0);
@@ -172,16 +283,19 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // U[q][s<tau], in Qrows/Urows for k_fold).  Loads are batched YB deep per
     // thread so the fill is one memory round trip, not one per element.
     const int KW = P.win;
-    const int nw = WIN ? S.nw : 0;
+    const int nw = WIN ? s_nw : 0;
     if (WIN && nw >= KW) {  // the host folds before this can happen
-        if (wg0 && tid == 0) st->status = ST_WINDOW_FULL;
+        if (wg0 && tid == 0) {
+            if (fresh) apply_deferred_tail(P, st, s_rec, s_tp);
+            st->status = ST_WINDOW_FULL;
+        }
         return;
     }
     const bool pend = WIN ? nw > 0 : it > 0;
     const int tau = nw - 1;  // pending pivot of the window
-    const int64_t qq = pend ? S.q : 0;
+    const int64_t qq = pend ? s_q : 0;
     const bool upd_y = !WIN && S.y_applied < it;
-    const double s_y = S.s_y;
+    const double s_y = s_sy;
     dbl2* yout = reinterpret_cast<dbl2*>(S.y_buf ? P.y0 : P.y1);
     // the pending pivot row: row q of the stored B^-1 (replicated storage), or
     // rbuf, staged by k_finalize_rs from the all-gather (row-sharded storage)
@@ -299,16 +413,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 syl = P.SY[lane];
                 if constexpr (SE) csl = P.se_cg[lane];
             }
-            syp = P.SY[tau];
+            syp = fresh ? s_sy : P.SY[tau];  // (fresh: workgroup 0 is writing SY[tau])
             if constexpr (SE) se_gp = P.se_cg[KW];
         }
     }
     double best = INFINITY, bw = 0.0, be = 0.0;
     int64_t bj = INT64_MAX;
-    const int64_t dvx_leave = S.leave;
-    const double dvx_wp = S.wp, dvx_aq = S.aq;
-    unsigned long long* const win = slot ? P.stamps + 20 : nullptr;
+    const int64_t dvx_leave = s_leave;
+    const double dvx_wp = s_wp, dvx_aq = s_aq;
+    unsigned long long* const win = (slot && !P.defer_price) ? P.stamps + 20 : nullptr;
     stamp_stream(win, true);
+    const unsigned long long t_pw2 = P.stamps ? rtime() : 0ull;  // the staging is in LDS
     const int nlist = nb;
     const int stride = gridDim.x * WAVES;
     // candidate update shared by every mode: Devex key, then the argmin
@@ -387,7 +502,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     bool have = pre && !unit_col(j0);
     for (int idx = idx0; idx < nlist; idx += stride) {
         const bool first = idx == idx0;
-        const int64_t j = first ? j0 : (int64_t)P.nb_list[idx];
+        const int64_t j = first ? j0 : nbl(idx);
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
         double wv = 0.0;
         if (WIN && pend && lane < tau) wv = P.Wt[j * KW + lane];
@@ -555,7 +670,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         // next column's first chunks in flight during this column's reduction
         const int nidx = idx + stride;
-        const int64_t jn = nidx < nlist ? (int64_t)P.nb_list[nidx] : 0;
+        const int64_t jn = nidx < nlist ? nbl(nidx) : 0;
         have = nidx < nlist && L2 >= CH * 64 && !unit_col(jn);
         if (have) {
             const dbl2* cn = reinterpret_cast<const dbl2*>(P.A + jn * L);
@@ -589,16 +704,16 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if (lane == 0) red[wave] = PricePartial{best, bj, bw, be};
     __syncthreads();
     if (P.stamps && tid == 0 && blockIdx.x < 4096) {  // diagnostics: this workgroup's start and end
-        unsigned long long* pw = P.stamps + 32 + 4 * 4096 + 2 * (int64_t)blockIdx.x;
+        unsigned long long* pw = P.stamps + STAMP_PRICE + (it & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x;
         pw[0] = t_pw0;
         pw[1] = rtime();
+        pw[2] = t_pw1;
+        pw[3] = t_pw2;
     }
     if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
         if (tid == 0) {
-            PricePartial w = red[0];
-            for (int i = 1; i < WAVES; ++i)
-                if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
-            P.price_partials[blockIdx.x] = w;
+            P.price_partials[blockIdx.x] = red[best_wave<WAVES>(red)];
+            if (fresh && blockIdx.x == 0) apply_deferred_tail(P, st, s_rec, s_tp);
         }
         return;
     }
@@ -611,9 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         // partial; its earlier window entries were written by earlier kernels.
         const uint32_t tag = (uint32_t)(it + 1);
         if (wave == 0) {
-            PricePartial w = red[0];
-            for (int i = 1; i < WAVES; ++i)
-                if (argmin_better(red[i].val, red[i].idx, w.val, w.idx)) w = red[i];
+            const PricePartial w = red[best_wave<WAVES>(red)];
             if (lane < PRICE_WORDS) {
                 const int f = lane >> 1;
                 const uint64_t u = f == 0 ? (uint64_t)__double_as_longlong(w.val)
@@ -763,28 +876,39 @@ __device__ double block_sum(double a, double* sa) {
 // over 64 workgroups are then 512 contiguous bytes; with 64-byte records every
 // lane's field load was a line of its own (7 x 512 line requests from the one
 // CU that runs the tail).
+// PLAIN: read only after the kernel boundary (the deferred tail)
+template <bool PLAIN = false>
 __device__ __forceinline__ void upd_publish(const Params& P, int g, const UpdPartial& w) {
     double* const s = P.upd_soa + g;
     const int64_t c = P.upd_cap;
-    st_agent(&s[0 * c], w.theta);
-    st_agent(reinterpret_cast<int64_t*>(&s[1 * c]), w.idx);
-    st_agent(reinterpret_cast<int64_t*>(&s[2 * c]), w.nonpos);
-    st_agent(&s[3 * c], w.T);
-    st_agent(&s[4 * c], w.a_w);
-    st_agent(&s[5 * c], w.cb_w);
-    st_agent(reinterpret_cast<int64_t*>(&s[6 * c]), w.bix_w);
+    auto st = [](auto* q, auto v) {
+        if constexpr (PLAIN) *q = v;
+        else st_agent(q, v);
+    };
+    st(&s[0 * c], w.theta);
+    st(reinterpret_cast<int64_t*>(&s[1 * c]), w.idx);
+    st(reinterpret_cast<int64_t*>(&s[2 * c]), w.nonpos);
+    st(&s[3 * c], w.T);
+    st(&s[4 * c], w.a_w);
+    st(&s[5 * c], w.cb_w);
+    st(reinterpret_cast<int64_t*>(&s[6 * c]), w.bix_w);
 }
+// PLAIN: after a kernel boundary (the deferred tail) the partials are read
+// with ordinary loads, so each XCD's L2 serves its workgroups after the first
+// miss; inside the producing launch they need agent-scope loads
+template <bool PLAIN = false>
 __device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g) {
     const double* const s = P.upd_soa + g;
     const int64_t c = P.upd_cap;
+    auto ld = [](const auto* q) { return PLAIN ? *q : ld_agent(q); };
     UpdPartial v;
-    v.theta = ld_agent(&s[0 * c]);
-    v.idx = ld_agent(reinterpret_cast<const int64_t*>(&s[1 * c]));
-    v.nonpos = ld_agent(reinterpret_cast<const int64_t*>(&s[2 * c]));
-    v.T = ld_agent(&s[3 * c]);
-    v.a_w = ld_agent(&s[4 * c]);
-    v.cb_w = ld_agent(&s[5 * c]);
-    v.bix_w = ld_agent(reinterpret_cast<const int64_t*>(&s[6 * c]));
+    v.theta = ld(&s[0 * c]);
+    v.idx = ld(reinterpret_cast<const int64_t*>(&s[1 * c]));
+    v.nonpos = ld(reinterpret_cast<const int64_t*>(&s[2 * c]));
+    v.T = ld(&s[3 * c]);
+    v.a_w = ld(&s[4 * c]);
+    v.cb_w = ld(&s[5 * c]);
+    v.bix_w = ld(reinterpret_cast<const int64_t*>(&s[6 * c]));
     v.pad = 0;
     return v;
 }
@@ -852,9 +976,9 @@ __device__ __forceinline__ void upd_clear_tagged(const Params& P, int g) {
 // (v4:317-325), carrying the winner's scalars.  One dependent round trip
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
 // order is fixed for a given launch geometry.
-template <int BLOCK>
-__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag = 0,
-                                             bool* timed_out = nullptr) {
+template <int BLOCK, bool PLAIN>
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag,
+                                             bool* timed_out) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     UpdPartial w = upd_empty();
@@ -872,8 +996,8 @@ __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, i
         if (!ok) *timed_out = true;  // (a benign race: every writer stores true)
     } else {
         // every slot's seven fields are loaded before any is used (one round trip)
-        w = (tid < nparts) ? upd_fetch(P, tid) : upd_empty();
-        for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch(P, g));
+        w = (tid < nparts) ? upd_fetch<PLAIN>(P, tid) : upd_empty();
+        for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch<PLAIN>(P, g));
     }
     // wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
     // winner's scalars come from its lane by readlane
@@ -931,12 +1055,14 @@ __host__ __device__ inline bool upd_xlds(const Params& P) {
 // Scalars of the bookkeeping that only depend on the entering column, loaded
 // by every k_update workgroup at its start so the last one's tail does not
 // wait on a chain of dependent global loads.
+// (32-bit flags: with bool members the partly-assigned struct was kept in
+// scratch rather than registers)
 struct TailPre {
-    bool valid;
+    int32_t valid;
     double c_p;
     int32_t cnt, kp, last;
     double wp;  // Devex: the entering column's weight
-    bool has_e;
+    int32_t has_e;
     double e_enter;  // deferred pricing tail: the entering column's reduced cost
     int32_t nw;      // eta window: pivots in the window (stable until the tail)
 };
@@ -947,7 +1073,7 @@ __device__ __forceinline__ void tail_last(const Params& P, TailPre* t) {
 }
 
 __device__ __forceinline__ TailPre tail_prefetch(const Params& P, int32_t nw, int32_t cnt, int64_t p) {
-    TailPre t{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
+    TailPre t{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (p < 0 || p >= P.n) return t;
     if (P.win) t.nw = nw;
     t.c_p = P.c[p];
@@ -1034,6 +1160,44 @@ __device__ void update_tail(const Params& P, DevState* st, int64_t p, double min
     const double e_rep = !P.devex ? min_e : (pre && pre->has_e ? pre->e_enter : *P.dvx_e);
     pivot_bookkeeping(P, st, p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, c_p), e_rep, it, pre);
     tail_mark(P, 1, tm);
+}
+
+// The deferred tail's bookkeeping from the reduced partial t (update_tail's,
+// with the FTRAN pass's TailRec in place of its prefetched scalars).  One
+// thread: workgroup 0 of the next pricing pass, or k_apply_tail.
+__device__ __forceinline__ void apply_deferred_tail(const Params& P, DevState* st, const TailRec& R,
+                                                    const UpdPartial& t) {
+    const int64_t q = t.idx;
+    if (t.nonpos == P.m || q < 0 || q >= P.m) {  // Unbounded (v4:319-322)
+        st->p = R.p;
+        st->min_e = R.e_rep;
+        st->status = ST_UNBOUNDED;
+        return;
+    }
+    const TailPre pre{1, R.c_p, R.cnt, R.kp, R.last, R.wp, 0, 0.0, R.nw};
+    pivot_bookkeeping(P, st, R.p, q, t.bix_w, t.a_w, y_scalar(t.T, t.a_w, t.cb_w, R.c_p), R.e_rep, R.it, &pre);
+}
+
+// A pending deferred tail applied on its own (before a fold, at the end of a
+// batch of passes, before any readback): one workgroup of 512 threads, the
+// reduction shape of the FTRAN tail and of k_price (the same bits).  Clears
+// the record either way.
+__global__ __launch_bounds__(512) void k_apply_tail(Params P) {
+    DevState* st = P.st;
+    const TailRec R = *P.trec;
+    if (!R.fresh) return;
+    if (R.it == st->iter) {  // not yet applied by a pricing pass
+        __shared__ UpdPartial s_ured[8];
+        const UpdPartial t = reduce_update_partials<512, true>(P, s_ured, P.tail_parts);
+        if (threadIdx.x == 0) apply_deferred_tail(P, st, R, t);
+    }
+    if (threadIdx.x == 0) P.trec->fresh = 0;
+}
+
+hipError_t launch_apply_tail(const Params& P, hipStream_t s) {
+    if (!P.trec) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_tail, dim3(1), dim3(512), 0, s, P);
+    return hipGetLastError();
 }
 
 template <int BLOCK>
@@ -1315,7 +1479,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
     for (int u = 0; u < R; ++u)
         ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
-    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
+    TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
     if (P.defer_price) {
         tpre.has_e = true;
@@ -1686,8 +1850,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 // column list, A_p[i] and the winner's window coefficients Wt[p][.].  (In
 // k_update the chunks past the first waited for S, A_p's gather for the row
 // prefetch, and alpha for A_p's gather.)
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
+// (launch bounds: 4 waves per SIMD, <= 128 VGPRs, so two 512-thread
+// workgroups share a CU and the C3 grid, 512 workgroups, is resident at once:
+// at 130 VGPRs it ran in two rounds, 11.6 -> 17.0 us)
+template <int BLOCK, bool DEFER>
+__global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     DevState* st = P.st;
     using Lds = UpdLds<BLOCK>;
     constexpr int WAVES = BLOCK / 64;
@@ -1730,6 +1897,8 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     Sv.nw = st->nw;
     const int Sbc = P.bc_n[0];
     const int64_t ldc = P.bc_n[1];  // compact row pitch (k_bc_list)
+    // (the entry clock goes here: taken first, its kernel-argument test ahead
+    // of the loads reordered them, 11.7 -> 13.0 us)
     const unsigned long long t_wg_entry = P.stamps ? rtime() : 0ull;
     // the compact row's first NCH chunks (S and the state are scalars: one wait)
     const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + ic * ldc);
@@ -1779,12 +1948,16 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
         }
     }
-    if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) return;
+    if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) {
+        if (DEFER && blockIdx.x == 0 && tid == 0) P.trec->fresh = 0;  // no pivot: nothing deferred
+        return;
+    }
     // (diagnostics: plain per-workgroup stores only -- the atomic phase
     // stamps of the other kernels, 512 workgroups on one address, would
     // themselves delay this kernel's waits)
     unsigned long long* const slot = nullptr;
-    unsigned long long* const wgt = (P.stamps && tid == 0) ? P.stamps + 32 + 4 * (int64_t)blockIdx.x : nullptr;
+    unsigned long long* const wgt =
+        (P.stamps && tid == 0) ? P.stamps + STAMP_FTRAN + (Sv.iter & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x : nullptr;
     if (wgt) {
         wgt[0] = t_wg_entry;
         wgt[1] = rtime();
@@ -1794,6 +1967,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             st->p = p;
             st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
             st->status = ST_OPTIMAL;
+            if (DEFER) P.trec->fresh = 0;
         }
         return;
     }
@@ -1809,8 +1983,20 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
     const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
                                    : P.Wt + p * KW;
     const double wlr = wrec[lane < KW ? lane : 0];
-    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0, 0};
-    if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
+    TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
+    if (!DEFER && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
+    // deferred tail: workgroup 0 records tail_prefetch's scalars (as scalars:
+    // the record written from tpre kept tpre in scratch)
+    double rc_p = 0.0, rwp = 0.0;
+    int32_t rkp = -1, rlast = -1;
+    if (DEFER && blockIdx.x == 0 && tid == 0) {
+        rc_p = P.c[p];
+        if (owns_col(P, p)) {
+            rkp = P.nb_pos[p];
+            rlast = P.nb_list[Sv.nb_count - 1];
+        }
+        if (P.devex) rwp = P.W[p];
+    }
     if (P.defer_price) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
@@ -1870,32 +2056,26 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             }
         }
     }
-    // ---- window terms, the pending eta column, s_x, the basic Wt entries
+    // ---- window terms, the pending eta column, s_x (the row's stores wait
+    // until the partial is out: a wave's vmcnt counts its stores, so stores
+    // issued before the merge put their write acknowledgements on the path
+    // to the publish)
     const double wl = lane < Sv.nw ? wlr : 0.0;
     double acc = 0.0;
     if (rowv) {
         const double cu = lane < tau ? urow : (lane == tau ? ei : 0.0);
         acc = fma(cu, wl, a);
-        if (pend && lane == 0) P.U[i * KW + tau] = ei;
     }
     double sxw = 0.0;
-    if (pend) {
-        sxw = sx_x + wave_sum(lane < tau ? mul_nc(sxw_u, sxw_w) : 0.0);
-        if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
-        if (lane == 0 && rowv) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
-    }
+    if (pend) sxw = sx_x + wave_sum(lane < tau ? mul_nc(sxw_u, sxw_w) : 0.0);
     const double s_x = upd_x ? sxw : 0.0;
 
     // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partial
     UpdPartial wp = upd_empty();
+    double al = 0.0, xb = xb0;
     if (rowv) {
-        const double al = wave_sum(acc);
-        double xb = xb0;
+        al = wave_sum(acc);
         if (upd_x) xb = fma(s_x, ei, xb);
-        if (lane == 0) {
-            a_new[i] = al;
-            if (upd_x) P.x_b[i] = xb;
-        }
         const bool pos = al > P.piv_tol;
         const double th = ratio_key(P, xb, al);
         wp.nonpos += !pos;
@@ -1908,6 +2088,20 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             wp.bix_w = bix;
         }
     }
+    // alpha_i (read back by the next pass / k_flush), x_b, the pending eta
+    // entry into U, and the basic columns' Wt entries (s_x in Wt[n])
+    auto store_row = [&]() {
+        if (rowv && lane == 0) {
+            if (pend) P.U[i * KW + tau] = ei;
+            a_new[i] = al;
+            if (upd_x) P.x_b[i] = xb;
+            if (pend) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
+        }
+        if (pend && blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
+    };
+    // (the counted and tagged hand-offs: stores first, as their tail's polls
+    // would otherwise wait behind them; deferred: after the publish)
+    if constexpr (!DEFER) store_row();
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
     if (lane == 0) red[wave] = wp;
@@ -1918,6 +2112,29 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
             for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
             upd_publish(P, blockIdx.x, w);
         }
+        return;
+    }
+    if constexpr (DEFER) {  // the next pricing pass (or k_apply_tail) reduces the partials
+        if (tid == 0) {
+            UpdPartial w = red[0];
+            for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
+            upd_publish<true>(P, blockIdx.x, w);
+            if (wgt) wgt[3] = rtime();
+            if (blockIdx.x == 0) {
+                TailRec* r = P.trec;
+                r->it = it;
+                r->p = p;
+                r->e_rep = !P.devex ? min_e : (P.defer_price ? e_enter : *P.dvx_e);
+                r->c_p = rc_p;
+                r->wp = rwp;
+                r->cnt = Sv.nb_count;
+                r->kp = rkp;
+                r->last = rlast;
+                r->nw = Sv.nw;
+                r->fresh = 1;
+            }
+        }
+        store_row();
         return;
     }
     if (P.upd_tag) {  // tagged hand-off to the last workgroup
@@ -1932,6 +2149,7 @@ __global__ __launch_bounds__(BLOCK) void k_ftran_bc(Params P) {
         const unsigned long long t_tail = slot ? rtime() : 0;
         update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre, tag);
         stamp_tail(slot, t_tail, win);
+        if (wgt) P.stamps[STAMP_TAIL + (it & 1)] = rtime();  // the bookkeeping is issued
         return;
     }
     if (tid == 0) {
@@ -2015,7 +2233,7 @@ __global__ __launch_bounds__(BLOCK) void k_tab_update(Params P) {
         if (blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
     }
     const double s_x = upd_x ? sxw : 0.0;
-    TailPre tpre{false, 0.0, 0, -1, -1, 0.0, false, 0.0};
+    TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (tid == 0 && !P.split_tail) tpre = tail_prefetch(P, st->nw, st->nb_count, p);
     if (P.defer_price) {
         tpre.has_e = true;
@@ -2450,6 +2668,7 @@ __global__ void k_reset(Params P) {
         if (P.xw) P.xw[i] = P.b[i];  // B_w = I
     }
     for (int64_t k = t0; k < ARR_GROUPS * ARR_LINES * ARR_STRIDE; k += stride) P.arrive[k] = 0u;
+    if (P.trec && t0 == 0) P.trec->fresh = 0;
     if (P.upd_tag)
         for (int64_t k = t0; k < UPD_WORDS * P.upd_cap; k += stride) P.upd_tag[k] = 0ull;
     if (P.price_tag)
@@ -2577,19 +2796,27 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
     return hipGetLastError();
 }
 
-template <int BLOCK>
-static hipError_t launch_ftran_bc(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+template <int BLOCK, bool DEFER>
+static hipError_t launch_ftran_bc_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = UpdLds<BLOCK>::bytes + (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8;
     if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK>),
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK, DEFER>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         if (e != hipSuccess) return e;
     }
     if (e0 || e1)
-        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     else
-        hipLaunchKernelGGL((k_ftran_bc<BLOCK>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER>), dim3(grid), dim3(BLOCK), lds, s, P);
     return hipGetLastError();
+}
+
+// deferred ratio-test tail: its own instantiation (no tail code, and the
+// tail's registers stay out of the hand-off kernel)
+template <int BLOCK>
+static hipError_t launch_ftran_bc(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    return P.defer_tail ? launch_ftran_bc_t<BLOCK, true>(P, grid, s, e0, e1)
+                        : launch_ftran_bc_t<BLOCK, false>(P, grid, s, e0, e1);
 }
 
 template <int BLOCK, int R>
@@ -2775,7 +3002,16 @@ static hipError_t launch_update_b(const Params& P, const UpdateCfg& c, hipStream
     return hipErrorInvalidValue;
 }
 
+// Diagnostic (SPX_DIAG_MARK=1 with stamps): a one-wave kernel before the
+// FTRAN launch records when it starts, splitting the pricing -> FTRAN
+// boundary into the pricing kernel's end and the FTRAN kernel's start
+__global__ __launch_bounds__(64) void k_mark(Params P) {
+    const unsigned long long now = rtime();
+    if (threadIdx.x == 0 && P.stamps) P.stamps[STAMP_TAIL + 2 + (P.st->iter & 1)] = now;
+}
+
 hipError_t launch_update(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (P.stamps && c.mark) hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, s, P);
     if (P.tab) {  // window tableau: k_tab_update, 256 rows per workgroup
         const size_t lds = UpdLds<256>::bytes;
         if (e0 || e1)

@@ -23,21 +23,35 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
         }                                                                                 \
     } while (0)
 
+__device__ double* g_wt;  // Wt-like side array (nc x 64 doubles)
+__device__ __forceinline__ double* wt_row(const double*, long j) { return g_wt + j * 64; }
+template <bool NT>
 __global__ __launch_bounds__(512) void k_cols(const double* __restrict__ A, long nc, long L2, long ld,
-                                              double* __restrict__ out, unsigned long long* __restrict__ tend) {
+                                              double* __restrict__ out, unsigned long long* __restrict__ tend,
+                                              double* __restrict__ scat, int scat_stride, int wt, int lds_n) {
+    extern __shared__ double lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long stride = (long)gridDim.x * 8;
     double acc = 0.0;
+    for (int k = threadIdx.x; k < lds_n; k += 512) lds[k] = (double)k;
+    __syncthreads();
     for (long j = (long)blockIdx.x * 8 + wave; j < nc; j += stride) {
         const dbl2* col = reinterpret_cast<const dbl2*>(A + j * ld);
+        if (scat && lane == 0) scat[j * scat_stride] = (double)j;  // one scattered store per column
+        if (wt) {  // the pricing pass's Wt pattern: read a 512 B row, write one entry of it
+            const double w = lane < 63 ? wt_row(A, j)[lane] : 0.0;
+            acc += w;
+            if (lane == 0) wt_row(A, j)[63] = acc;
+        }
         for (long k = lane; k < L2; k += 16 * 64) {
             dbl2 v[16];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) v[t] = __builtin_nontemporal_load(&col[k + t * 64]);
+            for (int t = 0; t < 16; ++t) v[t] = NT ? __builtin_nontemporal_load(&col[k + t * 64]) : col[k + t * 64];
 #pragma unroll
             for (int t = 0; t < 16; ++t) acc += v[t].x + v[t].y;
         }
     }
+    if (lds_n) acc += lds[(threadIdx.x * 7) % lds_n];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     __syncthreads();
     if (threadIdx.x == 0) tend[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -45,6 +59,11 @@ __global__ __launch_bounds__(512) void k_cols(const double* __restrict__ A, long
 }
 
 __global__ void k_t0(unsigned long long* t) { *t = __builtin_amdgcn_s_memrealtime(); }
+// the next kernel's first workgroup start (kernel boundary probe)
+__global__ void k_t1(unsigned long long* t) {
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) atomicMin(t, now);
+}
 
 int main(int argc, char** argv) {
     const long nc = argc > 1 ? atol(argv[1]) : 12288;
@@ -63,31 +82,60 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<unsigned long long> h(grid);
-    for (long pad : {0L, 64L, 128L, 256L, 0L, 64L}) {
-        const long ld = L + pad;
+    double* scat = nullptr;
+    CK(hipMalloc(&scat, (size_t)nc * 64 * 8));
+    double* wtp = nullptr;
+    CK(hipMalloc(&wtp, (size_t)nc * 64 * 8));
+    CK(hipMemset(wtp, 0, (size_t)nc * 64 * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_wt), &wtp, sizeof(wtp)));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cols<true>), hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024));
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cols<false>), hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024));
+    unsigned long long* t1 = nullptr;
+    CK(hipMalloc(&t1, 8));
+    // pad: column stride L + pad; sstride: one store per column at j * sstride
+    // doubles (0 = none) -- the next kernel's first workgroup start after the
+    // last workgroup's end is the kernel boundary
+    struct Case { long pad; int sstride; int nt; long ncols; int ev; int wt; int lds; };
+    for (Case cs : {Case{0, 0, 1, nc, 0, 0, 0}, Case{0, 0, 1, nc, 0, 1, 0}, Case{0, 0, 1, nc, 0, 0, 8192},
+                     Case{0, 0, 1, nc, 0, 0, 8320}, Case{0, 0, 1, nc, 0, 1, 8320}, Case{0, 0, 1, nc, 0, 0, 0}}) {
+        const long ld = L + cs.pad;
         float best = 1e9f;
         double spread = 0, p50 = 0;
+        std::vector<double> gaps;
         for (int r = 0; r < 20; ++r) {
             k_t0<<<1, 1>>>(t0);
+            const unsigned long long big = ~0ull;
+            CK(hipMemcpy(t1, &big, 8, hipMemcpyHostToDevice));
             CK(hipEventRecord(e0));
-            k_cols<<<grid, 512>>>(A, nc, L / 2, ld, out, tend);
-            CK(hipEventRecord(e1));
+            const size_t lb = (size_t)cs.lds * 8;
+            if (cs.nt)
+                k_cols<true><<<grid, 512, lb>>>(A, cs.ncols, L / 2, ld, out, tend, cs.sstride ? scat : nullptr, cs.sstride, cs.wt, cs.lds);
+            else
+                k_cols<false><<<grid, 512, lb>>>(A, cs.ncols, L / 2, ld, out, tend, cs.sstride ? scat : nullptr, cs.sstride, cs.wt, cs.lds);
+            if (cs.ev) CK(hipEventRecord(e1));
+            k_t1<<<512, 512>>>(t1);
+            if (!cs.ev) CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
+            CK(hipDeviceSynchronize());
             float ms = 0;
             CK(hipEventElapsedTime(&ms, e0, e1));
+            unsigned long long s0 = 0, s1 = 0;
+            CK(hipMemcpy(&s0, t0, 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&s1, t1, 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(h.data(), tend, grid * 8, hipMemcpyDeviceToHost));
+            std::sort(h.begin(), h.end());
+            gaps.push_back((double)(long long)(s1 - h[grid - 1]) * 0.01);
             if (ms < best) {
                 best = ms;
-                unsigned long long s0 = 0;
-                CK(hipMemcpy(&s0, t0, 8, hipMemcpyDeviceToHost));
-                CK(hipMemcpy(h.data(), tend, grid * 8, hipMemcpyDeviceToHost));
-                std::sort(h.begin(), h.end());
                 spread = (h[grid - 1] - h[0]) * 0.01;
                 p50 = (h[grid / 2] - s0) * 0.01;
             }
         }
-        const double gb = (double)nc * L * 8 / 1e9;
-        std::printf("{\"pad_doubles\": %ld, \"us\": %.2f, \"TBps\": %.3f, \"wg_end_spread_us\": %.2f, \"wg_end_p50_us\": %.2f}\n",
-                    pad, best * 1e3, gb / (best * 1e-3) / 1e3, spread, p50);
+        std::sort(gaps.begin(), gaps.end());
+        const double gb = (double)cs.ncols * L * 8 / 1e9;
+        std::printf("{\"wt\": %d, \"lds_doubles\": %d, \"ncols\": %ld, \"nontemporal\": %d, \"event_between\": %d, \"pad_doubles\": %ld, \"scatter_stride\": %d, \"us\": %.2f, \"TBps\": %.3f, "
+                    "\"wg_end_spread_us\": %.2f, \"wg_end_p50_us\": %.2f, \"boundary_us_p50\": %.2f}\n",
+                    cs.wt, cs.lds, cs.ncols, cs.nt, cs.ev, cs.pad, cs.sstride, best * 1e3, gb / (best * 1e-3) / 1e3, spread, p50, gaps[gaps.size() / 2]);
     }
     return 0;
 }

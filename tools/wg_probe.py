@@ -1,8 +1,10 @@
-"""Per-workgroup clock of the compact FTRAN pass (k_ftran_bc, stamps=True):
-when each workgroup starts, knows p, has A_p on the column list in LDS and
-publishes its partial, relative to the earliest start, over several eager
-passes.
-    python tools/wg_probe.py [--m 4096 --n 16384 --passes 6]"""
+"""Per-workgroup clock of two consecutive compact window passes (stamps=True,
+spx_wg_times), all on one clock (s_memrealtime, 100 MHz): pricing start /
+deferred ratio-test tail reduced / staging in LDS / end, FTRAN entry / p
+known / A_p in LDS / partial published, and the next pricing pass's start.
+Samples after several iterate() calls on the default (graph) dispatch;
+medians over samples, microseconds.
+    python tools/wg_probe.py [--m 4096 --n 16384 --samples 12 --step 7]"""
 import argparse
 import json
 import os
@@ -16,40 +18,49 @@ import simplex_method_gpu_amd as spx  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--m", type=int, default=4096)
 ap.add_argument("--n", type=int, default=16384)
-ap.add_argument("--passes", type=int, default=6)
+ap.add_argument("--samples", type=int, default=12)
+ap.add_argument("--step", type=int, default=7)
 ap.add_argument("--warm", type=int, default=70)
+ap.add_argument("--eager", action="store_true", help="one launch pair per iterate() call")
 a = ap.parse_args()
-rows, prow = [], []
-with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, graph_batch=-1) as ctx:
+kw = dict(graph_batch=-1) if a.eager else {}
+S = {}
+
+
+def put(k, v):
+    S.setdefault(k, []).append(float(v) * 0.01)  # ticks -> us
+
+
+with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
     ctx.iterate(a.warm)
-    for _ in range(a.passes):
-        ctx.iterate(1)
-        t = ctx.wg_times().astype(np.int64)
-        t = (t - t[:, 0].min()) * 0.01  # us
-        rows.append(t)
-        pt = ctx.price_wg_times().astype(np.int64)
-        prow.append((pt - pt[:, 0].min()) * 0.01)
-T = np.stack(rows)  # passes x grid x 4
-names = ["entry", "p_known", "ap_in_lds", "publish"]
-out = {}
-for k, nm in enumerate(names):
-    v = T[:, :, k]
-    out[nm] = {"p50": round(float(np.median(v)), 2), "p90": round(float(np.percentile(v, 90)), 2),
-               "max": round(float(v.max()), 2)}
-late = T[:, :, 3].mean(axis=0)
-order = np.argsort(-late)[:12]
-out["slowest_wg"] = [{"wg": int(g), "xcd": int(g % 8), "publish_us": round(float(late[g]), 2),
-                      "entry_us": round(float(T[:, g, 0].mean()), 2), "p_us": round(float(T[:, g, 1].mean()), 2),
-                      "ap_lds_us": round(float(T[:, g, 2].mean()), 2)} for g in order]
-xcd = [round(float(late[np.arange(len(late)) % 8 == x].mean()), 2) for x in range(8)]
-out["publish_mean_by_xcd"] = xcd
-half = len(late) // 2
-out["publish_mean_first_half_vs_second"] = [round(float(late[:half].mean()), 2), round(float(late[half:].mean()), 2)]
-PT = np.stack(prow)  # passes x price grid x 2
-pe = PT[:, :, 1]
-out["price_wg_end"] = {"p10": round(float(np.percentile(pe, 10)), 2), "p50": round(float(np.median(pe)), 2),
-                       "p90": round(float(np.percentile(pe, 90)), 2), "max": round(float(pe.max()), 2),
-                       "start_max": round(float(PT[:, :, 0].max()), 2)}
-out["price_wg_end_by_xcd"] = [round(float(pe.mean(axis=0)[np.arange(pe.shape[1]) % 8 == x].mean()), 2)
-                              for x in range(8)]
+    for _ in range(a.samples):
+        ctx.iterate(a.step)
+        w = ctx.wg_times()
+        # the earlier pass: the one whose pricing started first
+        lo, hi = (0, 1) if w[0]["price"][:, 0].min() < w[1]["price"][:, 0].min() else (1, 0)
+        A, B = w[lo], w[hi]
+        pa, fa, pb = (A["price"].astype(np.int64), A["ftran"].astype(np.int64), B["price"].astype(np.int64))
+        p0 = pa[:, 0].min()
+        f0 = fa[:, 0].min()
+        put("price_entry_spread", pa[:, 0].max() - p0)
+        put("price_entry_to_tail_reduced", np.median(pa[:, 2] - pa[:, 0]))
+        put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
+        put("price_staged_to_end_p50", np.median(pa[:, 1] - pa[:, 3]))
+        put("price_span", pa[:, 1].max() - p0)
+        put("price_end_spread", pa[:, 1].max() - pa[:, 1].min())
+        put("wg0_end_minus_p50_end", pa[0, 1] - np.median(pa[:, 1]))
+        put("price_end_to_ftran_entry", f0 - pa[:, 1].max())
+        put("ftran_entry_spread", fa[:, 0].max() - f0)
+        put("ftran_entry_to_p", np.median(fa[:, 1] - fa[:, 0]))
+        put("ftran_p_to_ap_lds", np.median(fa[:, 2] - fa[:, 1]))
+        put("ftran_ap_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
+        put("ftran_publish_max", fa[:, 3].max() - f0)
+        if A["tail"] > fa[:, 3].max():  # the FTRAN pass ran the tail itself
+            put("publish_max_to_tail", int(A["tail"]) - fa[:, 3].max())
+        put("ftran_publish_max_to_next_price", pb[:, 0].min() - fa[:, 3].max())
+        put("pass_total", pb[:, 0].min() - p0)
+out = {k: {"p50": round(float(np.median(v)), 2), "min": round(float(np.min(v)), 2),
+           "max": round(float(np.max(v)), 2)} for k, v in S.items()}
+out["config"] = {"m": a.m, "n": a.n, "eager": a.eager, "samples": a.samples,
+                 "defer_tail": os.environ.get("SPX_DEFER_TAIL", "1") != "0"}
 print(json.dumps(out, indent=1))
