@@ -243,6 +243,19 @@ __device__ __forceinline__ void upd_merge(UpdPartial& a, const UpdPartial& b) {
     a.nonpos += b.nonpos;
     a.T += b.T;
 }
+// the same merge with selects (the workgroup's final merge of its wave
+// partials: the branch form became a scalar branch per step on the uniform
+// LDS values, each step waiting for its own read)
+__device__ __forceinline__ void upd_merge_sel(UpdPartial& a, const UpdPartial& b) {
+    const bool t = argmin_better(b.theta, b.idx, a.theta, a.idx);
+    a.theta = t ? b.theta : a.theta;
+    a.idx = t ? b.idx : a.idx;
+    a.a_w = t ? b.a_w : a.a_w;
+    a.cb_w = t ? b.cb_w : a.cb_w;
+    a.bix_w = t ? b.bix_w : a.bix_w;
+    a.nonpos += b.nonpos;
+    a.T += b.T;
+}
 __device__ __forceinline__ UpdPartial upd_empty() { return UpdPartial{INFINITY, INT64_MAX, 0, 0.0, 0.0, 0.0, -1, 0}; }
 __device__ __forceinline__ UpdPartial upd_shfl_xor(const UpdPartial& v, int off) {
     UpdPartial o;

@@ -155,6 +155,10 @@ __device__ __forceinline__ int best_wave(const PricePartial* red) {
 template <int BLOCK, bool PLAIN = false>
 __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag = 0,
                                              bool* timed_out = nullptr);
+template <int BLOCK, bool PLAIN>
+__device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red);
+template <bool PLAIN = false>
+__device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g);
 // the deferred ratio-test tail's bookkeeping (TailRec; defined with the tail)
 __device__ __forceinline__ void apply_deferred_tail(const Params& P, DevState* st, const TailRec& R,
                                                     const UpdPartial& t);
@@ -195,12 +199,28 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // its own staging loads: vmcnt retires in order)
     __shared__ TailRec s_rec;
     __shared__ UpdPartial s_tp;
+#ifdef SPX_DIAG_FETCH_STAMP
+    unsigned long long t_fetch_all = 0;
+#endif
     if (P.defer_tail) {
+        // this thread's partial is requested beside the record, not behind
+        // its test (that was a second round trip)
+        UpdPartial w0 = tid < P.tail_parts ? upd_fetch<true>(P, tid) : upd_empty();
         const TailRec R = *P.trec;
         fresh = R.fresh != 0;
         if (fresh) {
             __shared__ UpdPartial s_ured[WAVES];
-            const UpdPartial t = reduce_update_partials<BLOCK, true>(P, s_ured, P.tail_parts);
+#ifdef SPX_DIAG_FETCH_STAMP  // timing probe: when the partials have arrived (stored as the pw[3] clock)
+            {
+                const int g0 = tid < P.tail_parts ? tid : 0;
+                const double th0 = P.upd_soa[g0];
+                const double bx0 = P.upd_soa[6 * P.upd_cap + g0];
+                asm volatile("" ::"v"(th0), "v"(bx0));
+                t_fetch_all = rtime();
+            }
+#endif
+            for (int g = tid + BLOCK; g < P.tail_parts; g += BLOCK) upd_merge(w0, upd_fetch<true>(P, g));
+            const UpdPartial t = reduce_partial_block<BLOCK, true>(w0, s_ured);
             const int64_t q = t.idx;
             const bool unb = t.nonpos == P.m || q < 0 || q >= P.m;
             if (blockIdx.x == 0 && tid == 0) {
@@ -708,7 +728,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         pw[0] = t_pw0;
         pw[1] = rtime();
         pw[2] = t_pw1;
+#ifdef SPX_DIAG_FETCH_STAMP
+        pw[3] = t_fetch_all;
+#else
         pw[3] = t_pw2;
+#endif
     }
     if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
         if (tid == 0) {
@@ -896,7 +920,7 @@ __device__ __forceinline__ void upd_publish(const Params& P, int g, const UpdPar
 // PLAIN: after a kernel boundary (the deferred tail) the partials are read
 // with ordinary loads, so each XCD's L2 serves its workgroups after the first
 // miss; inside the producing launch they need agent-scope loads
-template <bool PLAIN = false>
+template <bool PLAIN>
 __device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g) {
     const double* const s = P.upd_soa + g;
     const int64_t c = P.upd_cap;
@@ -976,29 +1000,13 @@ __device__ __forceinline__ void upd_clear_tagged(const Params& P, int g) {
 // (v4:317-325), carrying the winner's scalars.  One dependent round trip
 // (the sc1 partial loads); result broadcast to every thread.  The T sum's
 // order is fixed for a given launch geometry.
+// The workgroup's merge of its threads' ratio-test partials (the second half
+// of reduce_update_partials; the deferred tail calls it on partials it
+// requested at kernel entry)
 template <int BLOCK, bool PLAIN>
-__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag,
-                                             bool* timed_out) {
+__device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red) {
     constexpr int WAVES = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    UpdPartial w = upd_empty();
-    if (tag) {  // tagged hand-off: poll, then clear the consumed slots
-        bool ok = true;
-        for (int g = tid; g < nparts; g += BLOCK) {
-            UpdPartial v;
-            if (!upd_poll_tagged(P, g, tag, v)) {
-                ok = false;
-                break;
-            }
-            upd_merge(w, v);
-            upd_clear_tagged(P, g);
-        }
-        if (!ok) *timed_out = true;  // (a benign race: every writer stores true)
-    } else {
-        // every slot's seven fields are loaded before any is used (one round trip)
-        w = (tid < nparts) ? upd_fetch<PLAIN>(P, tid) : upd_empty();
-        for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch<PLAIN>(P, g));
-    }
     // wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
     // winner's scalars come from its lane by readlane
     double th = w.theta;
@@ -1023,11 +1031,51 @@ __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, i
     o.pad = 0;
     if (lane == 0) red[wave] = o;
     lds_barrier();
-    UpdPartial t = red[0];
+    if constexpr (PLAIN) {
+        // the deferred tail (k_price's prologue, k_apply_tail): every wave
+        // partial requested before a branch-free merge, and no closing
+        // barrier (the callers pass an LDS array of their own).  (In the
+        // FTRAN pass's tail the 8 partials in registers spilled.)
+        UpdPartial r[WAVES];
 #pragma unroll
-    for (int k = 1; k < WAVES; ++k) upd_merge(t, red[k]);
-    lds_barrier();
-    return t;
+        for (int k = 0; k < WAVES; ++k) r[k] = red[k];
+        UpdPartial t = r[0];
+#pragma unroll
+        for (int k = 1; k < WAVES; ++k) upd_merge_sel(t, r[k]);
+        return t;
+    } else {
+        UpdPartial t = red[0];
+#pragma unroll
+        for (int k = 1; k < WAVES; ++k) upd_merge(t, red[k]);
+        lds_barrier();
+        return t;
+    }
+}
+
+template <int BLOCK, bool PLAIN>
+__device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag,
+                                             bool* timed_out) {
+    constexpr int WAVES = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    UpdPartial w = upd_empty();
+    if (tag) {  // tagged hand-off: poll, then clear the consumed slots
+        bool ok = true;
+        for (int g = tid; g < nparts; g += BLOCK) {
+            UpdPartial v;
+            if (!upd_poll_tagged(P, g, tag, v)) {
+                ok = false;
+                break;
+            }
+            upd_merge(w, v);
+            upd_clear_tagged(P, g);
+        }
+        if (!ok) *timed_out = true;  // (a benign race: every writer stores true)
+    } else {
+        // every slot's seven fields are loaded before any is used (one round trip)
+        w = (tid < nparts) ? upd_fetch<PLAIN>(P, tid) : upd_empty();
+        for (int g = tid + BLOCK; g < nparts; g += BLOCK) upd_merge(w, upd_fetch<PLAIN>(P, g));
+    }
+    return reduce_partial_block<BLOCK, PLAIN>(w, red);
 }
 
 // LDS carve-up of k_update (dynamic, 16-byte aligned pieces)

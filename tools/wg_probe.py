@@ -44,8 +44,10 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
         f0 = fa[:, 0].min()
         put("price_entry_spread", pa[:, 0].max() - p0)
         put("price_entry_to_tail_reduced", np.median(pa[:, 2] - pa[:, 0]))
-        put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
-        put("price_staged_to_end_p50", np.median(pa[:, 1] - pa[:, 3]))
+        if os.environ.get("SPX_LIB", "").find("xfst") >= 0:  # (build with SPX_DIAG_FETCH_STAMP: clock 3 = partials in)
+            put("price_entry_to_partials_in", np.median(pa[:, 3] - pa[:, 0]))
+        else:
+            put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
         put("price_span", pa[:, 1].max() - p0)
         put("price_end_spread", pa[:, 1].max() - pa[:, 1].min())
         put("wg0_end_minus_p50_end", pa[0, 1] - np.median(pa[:, 1]))
