@@ -1984,12 +1984,35 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
         __shared__ PricePartial s_pw[WAVES];
         if (lane == 0) s_pw[wave] = PricePartial{bv, bj, 0.0, be};
         lds_barrier();
-        PricePartial t = s_pw[0];
-        for (int k = 1; k < WAVES; ++k)
-            if (argmin_better(s_pw[k].val, s_pw[k].idx, t.val, t.idx)) t = s_pw[k];
-        min_e = t.val;
-        p = t.idx;
-        e_enter = t.pad;
+        if constexpr (WAVES <= 8) {
+            // every wave's entry requested, then a branch-free scan (a branch
+            // per step on the uniform LDS values waited for each read in turn)
+            double pv[WAVES], pe[WAVES];
+            int64_t pj[WAVES];
+#pragma unroll
+            for (int k = 0; k < WAVES; ++k) {
+                pv[k] = s_pw[k].val;
+                pj[k] = s_pw[k].idx;
+                pe[k] = s_pw[k].pad;
+            }
+            min_e = pv[0];
+            p = pj[0];
+            e_enter = pe[0];
+#pragma unroll
+            for (int k = 1; k < WAVES; ++k) {
+                const bool b = argmin_better(pv[k], pj[k], min_e, p);
+                min_e = b ? pv[k] : min_e;
+                p = b ? pj[k] : p;
+                e_enter = b ? pe[k] : e_enter;
+            }
+        } else {  // (16 waves: the preloaded entries spilled)
+            PricePartial t = s_pw[0];
+            for (int k = 1; k < WAVES; ++k)
+                if (argmin_better(s_pw[k].val, s_pw[k].idx, t.val, t.idx)) t = s_pw[k];
+            min_e = t.val;
+            p = t.idx;
+            e_enter = t.pad;
+        }
     } else {
         for (int g = 0; g < P.nin; ++g) {
             const ArgMinEntry e = P.price_in[g * P.pr_stride];
