@@ -31,6 +31,7 @@ def put(k, v):
     S.setdefault(k, []).append(float(v) * 0.01)  # ticks -> us
 
 
+ends = []
 with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
     ctx.iterate(a.warm)
     for _ in range(a.samples):
@@ -61,8 +62,17 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
             put("publish_max_to_tail", int(A["tail"]) - fa[:, 3].max())
         put("ftran_publish_max_to_next_price", pb[:, 0].min() - fa[:, 3].max())
         put("pass_total", pb[:, 0].min() - p0)
+        ends.append((pa[:, 1] - p0) * 0.01)
 out = {k: {"p50": round(float(np.median(v)), 2), "min": round(float(np.min(v)), 2),
            "max": round(float(np.max(v)), 2)} for k, v in S.items()}
+E = np.stack(ends)  # samples x price grid: each workgroup's end, from the pass's first start
+g = np.arange(E.shape[1])
+out["price_end_by_xcd"] = [round(float(E[:, g % 8 == x].mean()), 2) for x in range(8)]
+out["price_end_by_wg_rank_corr"] = round(float(np.corrcoef(E[: len(E) // 2].mean(0), E[len(E) // 2:].mean(0))[0, 1]), 3)
+out["price_end_p10_p50_p90_max"] = [round(float(np.percentile(E, q)), 2) for q in (10, 50, 90, 100)]
+me = E.mean(0)
+out["price_slowest_wg"] = [[int(b), round(float(me[b]), 2), round(float(E[:, b].std()), 2)] for b in np.argsort(-me)[:12]]
+out["price_last_wg_counts"] = {int(k): int(v) for k, v in zip(*np.unique(E.argmax(1), return_counts=True))}
 out["config"] = {"m": a.m, "n": a.n, "eager": a.eager, "samples": a.samples,
                  "defer_tail": os.environ.get("SPX_DEFER_TAIL", "1") != "0"}
 print(json.dumps(out, indent=1))
