@@ -338,7 +338,9 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("k_loop pricing phase (in-kernel clock, workgroup 0), rank 0" if cfg.get("persistent")
-                           else "k_price (pricing GEMV + entering argmin), rank 0"),
+                           else "k_price (pricing GEMV + entering argmin"
+                           + (", prologue: the previous pivot's deferred ratio-test reduction" if cfg.get("defer_tail")
+                              else "") + "), rank 0"),
                 "achieved": price_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -348,7 +350,10 @@ def main():
                 "avg_launch_ms": ks["price_ms"],
             },
             "kernels": {
-                "k_update": {"what": "FTRAN (B_w read-only) + ratio test" if win else "rank-1 update (RMW) + FTRAN",
+                "k_update": {"what": ("rank-1 update (RMW) + FTRAN" if not win else
+                                      "FTRAN (B_w read-only) + ratio-test partials; the leaving argmin and the "
+                                      "bookkeeping run in the next k_price (deferred tail)" if cfg.get("defer_tail")
+                                      else "FTRAN (B_w read-only) + ratio test"),
                              "avg_launch_ms": ks["update_ms"], "algorithmic_bytes_per_launch": ks["update_bytes"],
                              "achieved_GBps": update_gbs, "frac": update_gbs / HBM_PEAK_GBS},
                 "k_fold": ({"avg_launch_ms": ks["fold_ms"], "launches_timed": ks["folds"],
