@@ -1037,7 +1037,17 @@ int set_slack_flags(spx_ctx* x) {
     x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
     if (x->bc_want && ident) {  // compact FTRAN operand (do_reset initialises it)
         Params& P = x->P;
-        SPX_TRY(x->alloc(&P.bc, (size_t)(m * x->L)));
+        // m x L more doubles (2.1 GB at C5): when they do not fit, the dense
+        // B_w stream that fit before is kept (every kernel tests P.bc)
+        void* d = nullptr;
+        if (hipMalloc(&d, (size_t)(m * x->L) * sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            x->bc_want = false;
+            return SPX_OK;
+        }
+        x->allocs.push_back(d);
+        HIP_TRY(hipMemsetAsync(d, 0, (size_t)(m * x->L) * sizeof(double), x->stream));
+        P.bc = static_cast<double*>(d);
         SPX_TRY(x->alloc(&P.rlist, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rmap, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rleft, (size_t)x->L));

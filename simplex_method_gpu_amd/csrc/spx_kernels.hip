@@ -28,6 +28,8 @@
 #include <hip/hip_ext.h>
 #include <math.h>
 
+#include <atomic>
+
 #include "spx_device.h"
 #include "spx_common.h"
 #include "spx_fold.h"
@@ -2849,13 +2851,17 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
                        ((WIN && BC) ? (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8
                                     : ((WIN && SPX_WIN_APLDS && P.L * 8 <= 65536) ? (size_t)P.L * 8 : 0)) +
                        ((!WIN && !RS && upd_xlds(P)) ? (size_t)P.L * 24 : 0);
-    if (lds > 65536) {  // once per instantiation (idempotent; not a stream operation)
-        static bool raised = false;
-        if (!raised) {
+    if (lds > 65536) {  // once per instantiation and device (idempotent; not a stream operation)
+        static std::atomic<uint64_t> raised{0};
+        int dev = 0;
+        const hipError_t ed = hipGetDevice(&dev);
+        if (ed != hipSuccess) return ed;
+        const uint64_t bit = 1ull << (dev & 63);
+        if (!(raised.load(std::memory_order_acquire) & bit)) {
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_update<BLOCK, R, RS, WIN, BNT, BC>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
             if (e != hipSuccess) return e;
-            raised = true;
+            raised.fetch_or(bit, std::memory_order_release);
         }
     }
     if (e0 || e1) {
