@@ -406,6 +406,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // eta window: the pending base row next to y when both fit; the tableau
     // pass stages nothing (wm 3)
     pc.wm = P.tab ? 3 : (!P.win ? 0 : ((pc.lds_y && 2 * ybytes + red_bytes <= lds_cap) ? 1 : 2));
+    if (pc.wm == 1 && env_on("SPX_PRICE_RGLOBAL")) pc.wm = 2;  // A/B: base row from L2 though it fits
     // steepest edge: B_w^T alpha beside y and the base row when all three fit
     if (P.steep) pc.wm = (pc.lds_y && 3 * ybytes + red_bytes <= lds_cap) ? 4 : 5;
     pc.lds_bytes = (pc.lds_y ? ybytes : 0) + ((pc.wm == 1 || pc.wm == 4) ? ybytes : 0) + (pc.wm == 4 ? ybytes : 0) +
