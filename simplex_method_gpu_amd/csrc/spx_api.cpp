@@ -1055,14 +1055,15 @@ int set_slack_flags(spx_ctx* x) {
         SPX_TRY(x->alloc(&P.bc_n, 4));
     }
     // deferred ratio-test tail (TailRec, spx_device.h): compact FTRAN passes
-    // (k_ftran_bc, one row per wave) with 512-thread pricing -- the reduction
-    // shape k_price, k_apply_tail and the FTRAN tail share -- on one rank, the
+    // (k_ftran_bc, one row per wave) with 512- or 256-thread pricing -- the
+    // reduction shape k_price (256 threads: two partials each,
+    // reduce_partial_pair), k_apply_tail and the FTRAN tail share -- on one rank, the
     // pricing tail deferred as well.  Measured at C3 (tools/fuse_est.py, the
     // timing-only estimate): 79.8 -> 73.9 us per pass.  SPX_DEFER_TAIL=0 keeps
     // the tail in the FTRAN pass.
     const UpdateCfg& uc = x->ucfg;
     if (x->P.bc && x->defer_ok && !x->persist && !x->P.steep && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
-        uc.block == 512 && x->pcfg.block == 512 && !env_off("SPX_DEFER_TAIL")) {
+        uc.block == 512 && (x->pcfg.block == 512 || x->pcfg.block == 256) && !env_off("SPX_DEFER_TAIL")) {
         SPX_TRY(x->alloc(&x->P.trec, 1));
         HIP_TRY(hipMemset(x->P.trec, 0, sizeof(TailRec)));
         x->P.tail_parts = uc.grid;

@@ -207,11 +207,18 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if (P.defer_tail) {
         // this thread's partial is requested beside the record, not behind
         // its test (that was a second round trip)
+        // 256-thread workgroups hold two threads' partials of the FTRAN
+        // tail's 512-thread shape (reduce_partial_pair: the same bits)
+        constexpr bool PAIR = BLOCK == 256;
         UpdPartial w0 = tid < P.tail_parts ? upd_fetch<true>(P, tid) : upd_empty();
+        UpdPartial w1 = upd_empty();
+        if constexpr (PAIR) {
+            if (tid + BLOCK < P.tail_parts) w1 = upd_fetch<true>(P, tid + BLOCK);
+        }
         const TailRec R = *P.trec;
         fresh = R.fresh != 0;
         if (fresh) {
-            __shared__ UpdPartial s_ured[WAVES];
+            __shared__ UpdPartial s_ured[PAIR ? 2 * WAVES : WAVES];
 #ifdef SPX_DIAG_FETCH_STAMP  // timing probe: when the partials have arrived (stored as the pw[3] clock)
             {
                 const int g0 = tid < P.tail_parts ? tid : 0;
@@ -221,8 +228,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 t_fetch_all = rtime();
             }
 #endif
-            for (int g = tid + BLOCK; g < P.tail_parts; g += BLOCK) upd_merge(w0, upd_fetch<true>(P, g));
-            const UpdPartial t = reduce_partial_block<BLOCK, true>(w0, s_ured);
+            UpdPartial t;
+            if constexpr (PAIR) {
+                for (int g = tid + 2 * BLOCK; g < P.tail_parts; g += 2 * BLOCK) {
+                    upd_merge(w0, upd_fetch<true>(P, g));
+                    if (g + BLOCK < P.tail_parts) upd_merge(w1, upd_fetch<true>(P, g + BLOCK));
+                }
+                t = reduce_partial_pair<BLOCK>(w0, w1, s_ured);
+            } else {
+                for (int g = tid + BLOCK; g < P.tail_parts; g += BLOCK) upd_merge(w0, upd_fetch<true>(P, g));
+                t = reduce_partial_block<BLOCK, true>(w0, s_ured);
+            }
             const int64_t q = t.idx;
             const bool unb = t.nonpos == P.m || q < 0 || q >= P.m;
             if (blockIdx.x == 0 && tid == 0) {
@@ -1005,12 +1021,9 @@ __device__ __forceinline__ void upd_clear_tagged(const Params& P, int g) {
 // The workgroup's merge of its threads' ratio-test partials (the second half
 // of reduce_update_partials; the deferred tail calls it on partials it
 // requested at kernel entry)
-template <int BLOCK, bool PLAIN>
-__device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red) {
-    constexpr int WAVES = BLOCK / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
-    // winner's scalars come from its lane by readlane
+// wave: DPP argmin on (theta, idx) and DPP sums (no LDS round trips); the
+// winner's scalars come from its lane by readlane
+__device__ __forceinline__ UpdPartial wave_reduce_partial(const UpdPartial& w) {
     double th = w.theta;
     int64_t ix = w.idx;
     double T = w.T;
@@ -1031,6 +1044,13 @@ __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, 
     o.cb_w = readlane_d(w.cb_w, wl);
     o.bix_w = readlane_l(w.bix_w, wl);
     o.pad = 0;
+    return o;
+}
+template <int BLOCK, bool PLAIN>
+__device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red) {
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const UpdPartial o = wave_reduce_partial(w);
     if (lane == 0) red[wave] = o;
     lds_barrier();
     if constexpr (PLAIN) {
@@ -1052,6 +1072,31 @@ __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, 
         lds_barrier();
         return t;
     }
+}
+
+// The 2*BLOCK-thread merge above (PLAIN) with BLOCK threads, bit for bit:
+// thread tid holds the partials of that shape's threads tid (wa) and
+// tid + BLOCK (wb), so its waves w and w + WAVES reduce the same lanes in the
+// same order, and the 2*WAVES wave partials merge in the same order.
+template <int BLOCK>
+__device__ __forceinline__ UpdPartial reduce_partial_pair(const UpdPartial& wa, const UpdPartial& wb,
+                                                          UpdPartial* red) {
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const UpdPartial oa = wave_reduce_partial(wa);
+    const UpdPartial ob = wave_reduce_partial(wb);
+    if (lane == 0) {
+        red[wave] = oa;
+        red[wave + WAVES] = ob;
+    }
+    lds_barrier();
+    UpdPartial r[2 * WAVES];
+#pragma unroll
+    for (int k = 0; k < 2 * WAVES; ++k) r[k] = red[k];
+    UpdPartial t = r[0];
+#pragma unroll
+    for (int k = 1; k < 2 * WAVES; ++k) upd_merge_sel(t, r[k]);
+    return t;
 }
 
 template <int BLOCK, bool PLAIN>

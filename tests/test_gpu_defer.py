@@ -43,12 +43,17 @@ def _run_chunks(ctx, chunks):
 CHUNKS = [1, 5, 63, 70, 7, 1, 130]
 
 
-@pytest.mark.parametrize("graph_batch", [0, -1])
-def test_deferred_tail_same_bits(spx, graph_batch):
+@pytest.mark.parametrize("graph_batch,price_block", [(0, 0), (-1, 0), (0, 256), (-1, 256)])
+def test_deferred_tail_same_bits(spx, graph_batch, price_block):
+    """price_block 256: each pricing thread holds two of the 512-thread
+    shape's partials (reduce_partial_pair), so the deferred tail keeps the
+    in-pass tail's bits with 256-thread pricing workgroups too."""
     m, n, seed = 2048, 6144, 3
     kw = dict(m=m, n=n, seed=seed, trace=sum(CHUNKS))
     if graph_batch < 0:
         kw["graph_batch"] = -1  # eager passes only
+    if price_block:
+        kw["price_block"] = price_block
     with _ctx(spx, True, **kw) as a, _ctx(spx, False, **kw) as b:
         assert a.config()["defer_tail"] == 1, a.config()
         assert b.config()["defer_tail"] == 0, b.config()
@@ -105,3 +110,20 @@ def test_deferred_tail_limit_and_resume(spx):
         sa, sb = a.state(), b.state()
     for key in ("b_ixs", "x_b", "y"):
         assert np.array_equal(sa[key], sb[key]), key
+
+
+def test_deferred_tail_price_block_256_same_bits_as_512(spx):
+    """Pricing geometry does not enter the bits: each column's dot is one
+    wave's, the entering argmin breaks ties by index, and the deferred
+    ratio-test tail reduces the same 512-thread shape with 256 or 512
+    threads.  Covers C3-shaped m = 4096 over two folds."""
+    kw = dict(m=4096, n=16384, seed=0, trace=140)
+    with _ctx(spx, True, price_block=256, **kw) as a, _ctx(spx, True, **kw) as b:
+        assert a.config()["defer_tail"] == 1 and b.config()["defer_tail"] == 1
+        assert a.config()["price_block"] == 256 and b.config()["price_block"] == 512
+        sa, pa, qa, za = _run_chunks(a, [3, 137])
+        sb, pb, qb, zb = _run_chunks(b, [3, 137])
+    assert np.array_equal(pa, pb) and np.array_equal(qa, qb)
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(sa[key], sb[key]), key
+    assert za == zb
