@@ -1057,12 +1057,16 @@ int set_slack_flags(spx_ctx* x) {
     // deferred ratio-test tail (TailRec, spx_device.h): compact FTRAN passes
     // (k_ftran_bc, one row per wave) with 512- or 256-thread pricing -- the
     // reduction shape k_price (256 threads: two partials each,
-    // reduce_partial_pair), k_apply_tail and the FTRAN tail share -- on one rank, the
-    // pricing tail deferred as well.  Measured at C3 (tools/fuse_est.py, the
+    // reduce_partial_pair), k_apply_tail and the FTRAN tail share -- on one rank
+    // with the pricing tail deferred as well; with G ranks (replicated B_w, so
+    // every rank holds the same FTRAN partials) the pricing tail stays in
+    // k_price for the exchange.  Measured at C3 (tools/fuse_est.py, the
     // timing-only estimate): 79.8 -> 73.9 us per pass.  SPX_DEFER_TAIL=0 keeps
     // the tail in the FTRAN pass.
     const UpdateCfg& uc = x->ucfg;
-    if (x->P.bc && x->defer_ok && !x->persist && !x->P.steep && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
+    const bool tail_ok = x->defer_ok || (x->use_comm && x->P.win && !x->P.split_tail && !x->P.row_shard &&
+                                         !(x->opts.flags & SPX_FLAG_PRICE_TAIL));
+    if (x->P.bc && tail_ok && !x->persist && !x->P.steep && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
         uc.block == 512 && (x->pcfg.block == 512 || x->pcfg.block == 256) && !env_off("SPX_DEFER_TAIL")) {
         SPX_TRY(x->alloc(&x->P.trec, 1));
         HIP_TRY(hipMemset(x->P.trec, 0, sizeof(TailRec)));
@@ -1330,11 +1334,14 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 spx_ctx* x = cs[g];
                 HIP_TRY(hipSetDevice(x->device));
                 const bool fold = fold_due(x);
+                if (fold && x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));
                 if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
                 advance_window(x, fold);
                 ++x->n_eager;
                 x->n_folds += fold ? 1 : 0;
-                HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
+                Params Pp = x->P;  // the deferred ratio-test tail (each rank's own FTRAN partials)
+                Pp.defer_tail = x->defer_tail ? 1 : 0;
+                HIP_TRY(launch_price(Pp, x->pcfg, x->stream, nullptr, nullptr));
                 HIP_TRY(hipEventRecord(x->ev_sent, x->stream));
             }
             for (int h = 0; h < G; ++h) {  // all-gather of the candidate records
@@ -1352,7 +1359,9 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
             for (int g = 0; g < G; ++g) {  // fused update; next pricing waits for every reader
                 spx_ctx* x = cs[g];
                 HIP_TRY(hipSetDevice(x->device));
-                HIP_TRY(launch_update(x->P, x->ucfg, x->stream, nullptr, nullptr));
+                Params Pp = x->P;
+                Pp.defer_tail = x->defer_tail ? 1 : 0;
+                HIP_TRY(launch_update(Pp, x->ucfg, x->stream, nullptr, nullptr));
                 if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
                 if (rs) HIP_TRY(hipEventRecord(x->ev_sent2, x->stream));
                 else
@@ -1382,6 +1391,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
         }
         for (int g = 0; g < G; ++g) {
             HIP_TRY(hipSetDevice(cs[g]->device));
+            if (cs[g]->defer_tail) HIP_TRY(launch_apply_tail(cs[g]->P, cs[g]->stream));  // the last pass's tail
             SPX_TRY(read_state(cs[g]));
         }
         for (int g = 1; g < G; ++g)

@@ -759,6 +759,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         return;
     }
+    // multi-rank passes (the pricing tail in this launch, for the exchange):
+    // workgroup 0 applies a deferred tail before it arrives; the fan-in below
+    // reads no state word the bookkeeping writes
+    if (fresh && blockIdx.x == 0 && tid == 0) apply_deferred_tail(P, st, s_rec, s_tp);
     if (P.price_tag) {
         // Tagged hand-off (as k_update's, upd_publish_tagged): wave 0
         // publishes the workgroup's partial as PRICE_WORDS {32-bit half, tag}

@@ -3,7 +3,8 @@ tests/test_gpu_mbox.py (not a test module).  The ranks exchange their
 mailbox handles through files in a directory, attach (spx_mbox_attach), run
 the pivots and store the state they reach.
 
-usage: python mbox_rank.py DIR RANK NRANKS M N SEED WINDOW K GRAPH_BATCH
+usage: python mbox_rank.py DIR RANK NRANKS M N SEED WINDOW K GRAPH_BATCH [SOLVE]
+(SOLVE 0: the state after K pivots only, no solve to the optimum)
 """
 import os
 import sys
@@ -17,7 +18,8 @@ import simplex_method_gpu_amd as spx  # noqa: E402
 
 
 def main():
-    d, rank, G, m, n, seed, window, k, gb = sys.argv[1], *map(int, sys.argv[2:])
+    d, rank, G, m, n, seed, window, k, gb = sys.argv[1], *map(int, sys.argv[2:10])
+    solve = int(sys.argv[10]) if len(sys.argv) > 10 else 1
     with spx.Context(m=m, n=n, seed=seed, rank=rank, nranks=G, window=window, graph_batch=gb) as ctx:
         h = ctx.mbox_export()
         tmp = os.path.join(d, f"h{rank}.tmp")
@@ -34,9 +36,14 @@ def main():
         ctx.mbox_attach(handles)
         st, piv = ctx.iterate(k)
         s = ctx.state(binv=True)
-        r = ctx.solve()
+        defer = ctx.config()["defer_tail"]
+        if solve:
+            r = ctx.solve()
+            z, pivots, status = r.z, r.pivots, int(r.status)
+        else:
+            z, pivots, status = ctx.objective(), piv, int(st)
         np.savez(os.path.join(d, f"r{rank}.npz"), piv=piv, b_ixs=s["b_ixs"], x_b=s["x_b"], y=s["y"],
-                 binv=s["binv"], z=r.z, pivots=r.pivots, status=int(r.status))
+                 binv=s["binv"], z=z, pivots=pivots, status=status, defer_tail=defer)
 
 
 if __name__ == "__main__":

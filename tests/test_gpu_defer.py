@@ -127,3 +127,31 @@ def test_deferred_tail_price_block_256_same_bits_as_512(spx):
     for key in ("b_ixs", "x_b", "y", "binv"):
         assert np.array_equal(sa[key], sb[key]), key
     assert za == zb
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_deferred_tail_shard_group(spx, G):
+    """Column-sharded in-process groups (replicated B_w, pricing tail in the
+    launch for the exchange) with the deferred ratio-test tail: identical to
+    the in-pass tail's group and to one rank, through two folds and mixed
+    iterate chunks."""
+    m, n, seed = 2048, 6144, 3
+    kw = dict(m=m, n=n, seed=seed, trace=sum(CHUNKS))
+    with _ctx(spx, True, **kw) as ref:
+        rs, rp, rq, rz = _run_chunks(ref, CHUNKS)
+    for defer in (True, False):
+        ctxs = [_ctx(spx, defer, rank=g, nranks=G, **kw) for g in range(G)]
+        try:
+            assert all(c.config()["defer_tail"] == (1 if defer else 0) for c in ctxs)
+            for k in CHUNKS:
+                spx.group_iterate(ctxs, k)
+            for c in ctxs:
+                s = c.state(binv=True)
+                p, q = c.trace()
+                assert np.array_equal(p, rp) and np.array_equal(q, rq), defer
+                for key in ("b_ixs", "x_b", "y", "binv"):
+                    assert np.array_equal(s[key], rs[key]), (defer, key)
+                assert c.objective() == rz
+        finally:
+            for c in ctxs:
+                c.close()

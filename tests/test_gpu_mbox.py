@@ -86,3 +86,39 @@ def test_mbox_processes_share_one_gpu(spx, oracle, tmp_path, G, window, graph_ba
         assert int(r["pivots"]) == rr.pivots == o.pivots
         assert float(r["z"]) == rr.z
         assert abs(rr.z - o.z) <= 1e-9 * abs(o.z)
+
+
+@pytest.mark.parametrize("graph_batch", [16, -1])
+def test_mbox_processes_deferred_tail(spx, tmp_path, graph_batch):
+    """m = 2048 (512-thread FTRAN workgroups, compact window passes): the
+    ranks run the deferred ratio-test tail -- each reduces its own replicated
+    FTRAN partials in the next pricing pass, whose pricing tail stays in the
+    launch for the exchange -- and reach the single-rank state bit for bit
+    through two folds."""
+    m, n, seed, k, G = 2048, 6144, 5, 140, 2
+    with spx.Context(m=m, n=n, seed=seed, window=64, persist=False) as ref:
+        assert ref.config()["defer_tail"] == 1
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+        rz = ref.objective()
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mbox_rank.py"), str(tmp_path), str(g), str(G),
+                               str(m), str(n), str(seed), "64", str(k), str(graph_batch), "0"],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=dict(os.environ)) for g in range(G)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for g, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {g}:\n{outs[g][-3000:]}"
+    for g in range(G):
+        r = np.load(tmp_path / f"r{g}.npz")
+        assert int(r["defer_tail"]) == 1
+        assert int(r["piv"]) == k
+        for key in ("b_ixs", "x_b", "y", "binv"):
+            assert np.array_equal(r[key], rs[key]), (g, key)
+        assert float(r["z"]) == rz
