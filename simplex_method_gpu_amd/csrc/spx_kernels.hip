@@ -352,6 +352,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // here is unconditional with a clamped index (rr is always a valid row),
     // so the fill waits for its own loads only, not for the A prefetch.
     constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
+    static_assert(CH >= 1 && CH <= 8, "the pipelined column loop consumes at most one 8-chunk batch of prefetch");
     const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
     dbl2 yv[YB], rv[YB], vv[YB];
     double uqrow = 0.0;  // U[q][tid] for Urows (window, workgroup 0)
