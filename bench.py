@@ -83,6 +83,10 @@ def parse():
                     help="skip the C4 column-sharded pricing block (pricing_c4)")
     ap.add_argument("--no-tableau", action="store_true",
                     help="skip the window-tableau measurement (the `tableau` block, one GPU only)")
+    ap.add_argument("--no-solve-to-optimum", action="store_true",
+                    help="skip the whole-solve block (the same LP from the slack basis to optimality)")
+    ap.add_argument("--no-steepest", action="store_true",
+                    help="skip the steepest-edge block (one GPU, eta window)")
     ap.add_argument("--comm1", action="store_true",
                     help="rehearsal on one GPU: run the multi-rank path (torch.distributed + RCCL "
                          "MINLOC) with a one-rank communicator")
@@ -218,11 +222,12 @@ def main():
                       "loop_ms_per_pass": lt["loop_ms"] / max(lt["loop_passes"], 1)}
         info1 = ctx.info()
         cols = ctx.ftran_cols()
+        comm = ctx.comm_info()
         ctx.close()
         return {"cfg": cfg, "dt": dt, "pivots": piv1 - piv0, "steps": steps, "lead": lead, "dispatch": delta,
                 "pt": pt, "lt": lt, "nb": 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"]),
                 "price_bytes": 0.5 * (info0["bytes_price"] + info1["bytes_price"]), "ftran_cols": cols,
-                "status": int(st)}
+                "status": int(st), "comm": comm}
 
     def kernel_split(run, window):
         """Per-kernel averages of an event-timed run, with algorithmic bytes."""
@@ -251,6 +256,20 @@ def main():
     cfg = main_run["cfg"]
     win = cfg["window"]
     value = main_run["pivots"] / main_run["dt"] if main_run["dt"] > 0 else 0.0
+    # evidence of what joined the job: every rank's own RCCL communicator
+    # size / rank, HIP device and PCI bus id, and graph capture, all-gathered
+    # and checked (rc != 0 on a mismatch: the line would not be a N-GPU run)
+    infos = [main_run["comm"]]
+    if multi:
+        infos = [None] * world
+        dist.all_gather_object(infos, main_run["comm"])
+    exchange = ("rccl" if args.minloc == "rccl" else "mbox") if multi else "none"
+    try:
+        spx.check_ranks(infos, world, exchange=exchange, distinct_gpus=not args.share_gpu)
+    except RuntimeError as e:
+        if multi:
+            dist.destroy_process_group()
+        raise SystemExit(f"bench.py: rank evidence check failed: {e}")
     # (2) the same window with per-dispatch hipEvents (eager): kernel split
     ev_run = timed_window(args.window, True)
     ks = kernel_split(ev_run, win)
@@ -281,6 +300,14 @@ def main():
     sharded = None
     if not args.no_sharded_pricing and (m, n) != CONFIGS["C4"]:
         sharded = sharded_pricing_block(make, reduce_max, reduce_sum, world, args)
+
+    to_opt = None
+    if not args.no_solve_to_optimum:
+        to_opt = solve_to_optimum_block(make, barrier, reduce_max, torch, args.window, main_run, value)
+
+    steep = None
+    if world == 1 and not multi and not args.no_steepest and win > 0:
+        steep = steepest_block(spx, torch, m, n, args, local)
 
     tab = None
     if world == 1 and not multi and not args.no_tableau:
@@ -324,6 +351,18 @@ def main():
                                   "B^-1 replicated"))
                                 if multi else "single GPU"),
                 "dispatch": describe_dispatch(main_run["dispatch"]),
+            },
+            "ranks": {
+                "world_size": world,
+                "exchange": exchange,
+                "rccl_nranks": infos[0]["rccl_nranks"],
+                "per_rank": [{"rank": i["rank"], "rccl_rank": i["rccl_rank"], "device": i["device"],
+                              "rccl_device": i["rccl_device"], "bus_id": i["bus_id"],
+                              "graph_captured": i["graph"], "graph_fallback": i["graph_fallback"]}
+                             for i in infos],
+                "checked": "spx.check_ranks: RCCL reports world_size ranks and each rank's own rank"
+                           + ("; distinct PCI bus ids" if not args.share_gpu else
+                              " (bus ids shared on purpose: --share-gpu rehearsal)"),
             },
             "timed_region": {
                 "pivots": main_run["pivots"],
@@ -384,6 +423,8 @@ def main():
                 "throughput_GBps": price_bytes_all / (minloc_ms_max * 1e-3) / 1e9 if minloc_ms_max > 0 else 0.0,
                 "max_rank_update_ms": update_ms_max,
             },
+            "solve_to_optimum": to_opt,
+            "steepest": steep,
             "explicit": explicit,
             "pricing_c4": sharded,
             "tableau": tab,
@@ -395,6 +436,100 @@ def main():
         print(json.dumps(out), flush=True)
     if multi:
         dist.destroy_process_group()
+
+
+def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, value):
+    """The whole solve of the headline LP: the default path from the slack
+    basis to optimality on the same clock as `value` (barrier + device sync on
+    both sides, max over ranks), dispatched as the library does it (captured
+    hipGraphs of whole windows plus a few eager passes at the ends of each
+    spx_iterate call).  `value` samples an early window, where the compact
+    FTRAN operand is narrow (S columns of B_w that are not unit); S grows over
+    the solve, and so does the FTRAN pass."""
+    ctx = make(False, window)
+    try:
+        cols0 = ctx.ftran_cols()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st, piv = ctx.iterate(0)
+        while st == 0:  # SolveStatus.MaxIter: not terminated yet
+            st, piv = ctx.iterate(4096)
+        torch.cuda.synchronize()
+        barrier()
+        dt = reduce_max([time.perf_counter() - t0])[0]
+        cols1 = ctx.ftran_cols()
+        z = ctx.objective()
+        ds = ctx.dispatch_stats()
+    finally:
+        ctx.close()
+    rate = piv / dt if dt > 0 else 0.0
+    return {"status": ["MaxIter", "OptimumFound", "Unbounded", "ThetaOverflow"][int(st)], "pivots": int(piv),
+            "seconds": dt, "iterations_per_s": rate, "z": z,
+            "ftran_cols_start": cols0, "ftran_cols_end": cols1,
+            "vs_value": rate / value if value > 0 else None,
+            "dispatch": f"{ds['graph_launches']} hipGraph replays ({ds['graph_passes']} passes) + "
+                        f"{ds['eager_passes']} eager passes; {ds['folds']} folds",
+            "note": "time to optimum from the slack basis (the v4:286-359 loop run to its exit, as the "
+                    "reference CLI times it at v4:456-471); `value` times one early window "
+                    f"(ftran_cols {main_run['ftran_cols']} there)"}
+
+
+def steepest_block(spx, torch, m, n, args, device):
+    """Exact steepest-edge pricing (SPX_PRICING_STEEPEST, Goldfarb-Reid
+    recurrence; README.md:16-17) on the same LP, one GPU: the per-pivot rate
+    over whole windows after the same warm-up (event-timed copy for the
+    pricing kernel with its third dot), and the whole solve from the slack
+    basis against Dantzig's pivot count."""
+    def ctx_():
+        return spx.Context(m=m, n=n, seed=args.seed, device=device, pricing=spx.PRICING_STEEPEST)
+
+    def window_run(timing):
+        with spx.Context(m=m, n=n, seed=args.seed, device=device, pricing=spx.PRICING_STEEPEST,
+                         timing=timing) as ctx:
+            cfg = ctx.config()
+            per = max(cfg["window"] - 1, 1)
+            steps = per * max(1, -(-args.steps // per))
+            ctx.iterate(args.warmup)
+            ds = ctx.dispatch_stats()
+            if ds["window"] and ds["window_pos"] < ds["window"]:
+                ctx.iterate(ds["window"] - ds["window_pos"])
+            if timing:
+                ctx.pass_times()
+                ctx.loop_times()
+            _, p0 = ctx.iterate(0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, p1 = ctx.iterate(steps)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            pt = ctx.pass_times() if timing else None
+            info = ctx.info()
+        return cfg, dt, p1 - p0, pt, info
+
+    cfg, dt, piv, _, info = window_run(False)
+    _, dt_e, piv_e, pt, _ = window_run(True)
+    passes = max(pt["passes"], 1)
+    price_ms = pt["price_ms"] / passes
+    with ctx_() as ctx:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st, tot = ctx.iterate(0)
+        while st == 0:
+            st, tot = ctx.iterate(4096)
+        torch.cuda.synchronize()
+        sdt = time.perf_counter() - t0
+        z = ctx.objective()
+    return {"value": piv / dt if dt > 0 else 0.0, "unit": "iterations/s",
+            "ms_per_step": 1e3 * dt / max(piv, 1), "steps": piv,
+            "k_price_ms": price_ms, "k_price_bytes": info["bytes_price"],
+            "k_price_GBps": info["bytes_price"] / (price_ms * 1e-3) / 1e9 if price_ms > 0 else 0.0,
+            "k_update_ms": pt["update_ms"] / passes,
+            "event_timed_ms_per_step": 1e3 * dt_e / max(piv_e, 1),
+            "solve": {"status": ["MaxIter", "OptimumFound", "Unbounded", "ThetaOverflow"][int(st)],
+                      "pivots": int(tot), "seconds": sdt, "z": z},
+            "representation": f"eta window {cfg['window']}, two-kernel passes; k_price carries a third "
+                              "dot on the A stream (B_w^T alpha beside y_w and the base row)"}
 
 
 def sharded_pricing_block(make, reduce_max, reduce_sum, world, args):

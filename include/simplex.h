@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 5
+#define SPX_ABI_VERSION 6
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -208,6 +208,21 @@ void spx_destroy(spx_ctx* ctx);
 int spx_comm_unique_id(uint8_t id[SPX_COMM_ID_BYTES]);
 int spx_attach_comm(spx_ctx* ctx, const uint8_t id[SPX_COMM_ID_BYTES]);
 
+/* Evidence of what actually joined the exchange (no reference counterpart:
+ * the reference is one process on one GPU).  out[0] = ranks the attached RCCL
+ * communicator reports (ncclCommCount; -1 when none is attached), out[1] =
+ * this rank in it (ncclCommUserRank; -1), out[2] = the HIP device RCCL bound
+ * (ncclCommCuDevice; -1), out[3] = the context's HIP device ordinal, out[4] =
+ * 1 when loop passes replay captured hipGraphs (the all-gathers inside them),
+ * 0 when they run eagerly, out[5] = 1 when a capture with RCCL calls failed
+ * and the context fell back to eager passes, out[6] = opts.nranks, out[7] =
+ * opts.rank.  bus_id: the context device's PCI bus id (hipDeviceGetPCIBusId,
+ * NUL-terminated).  Whether graphs are used is known once the first batch
+ * has been captured (the first spx_iterate long enough for one). */
+#define SPX_COMM_INFO_FIELDS 8
+#define SPX_BUS_ID_BYTES 64
+int spx_comm_info(spx_ctx* ctx, int32_t out[SPX_COMM_INFO_FIELDS], char bus_id[SPX_BUS_ID_BYTES]);
+
 /* Peer mailboxes: the pricing MINLOC exchange (the RCCL all-gather of the
  * candidate records after src/v4_cub_reduction.cu:294-302's argmin) as direct
  * stores into every rank's device mailbox over xGMI, one small kernel per pass
@@ -325,7 +340,12 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
  * (latest stream end -> last ticket), price prologue, price drain;
  * out[13..17] = the update kernel's workgroup 0, from its start to: status
  * read, entering column known, row stream start, its wave 0's stream end,
- * partial published.  Resets. */
+ * partial published.  Resets.
+ * Loop passes that defer the pricing tail (window passes and explicit passes
+ * at m <= 2048 on one rank, Params::defer_price) have no pricing ticket, so
+ * out[0], out[1], out[11] and out[12] stay 0 for them; the per-workgroup
+ * clocks of spx_wg_times cover those passes.  The step-wise API
+ * (spx_price / spx_pivot) keeps the pricing tail and fills every slot. */
 #define SPX_PHASES 18
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 

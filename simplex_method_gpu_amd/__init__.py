@@ -23,7 +23,7 @@ import numpy as np
 from ._lib import SimplexError, SpxOpts, check, load
 
 __all__ = ["SolveStatus", "SolveResult", "Context", "solve", "read_lp", "comm_unique_id",
-           "shard_range", "minloc_merge", "group_iterate", "group_sync",
+           "shard_range", "minloc_merge", "group_iterate", "group_sync", "check_ranks",
            "SimplexError", "FLAG_TIMING", "RATIO_REFERENCE", "RATIO_GUARDED", "RATIO_HARRIS",
            "PRICING_DANTZIG", "PRICING_DEVEX", "PRICING_STEEPEST"]
 
@@ -117,6 +117,26 @@ def group_sync(ctxs):
     check(load().spx_group_sync(arr, len(ctxs)))
 
 
+def check_ranks(infos, world: int, exchange: str = "rccl", distinct_gpus: bool = True):
+    """Validate the all-gathered :meth:`Context.comm_info` of every rank of a
+    job of ``world`` processes; raises ``RuntimeError`` naming the mismatch.
+    RCCL exchange: every communicator reports ``world`` ranks and rank r is
+    RCCL's rank r.  Always: rank r was created as rank r of ``world``; and,
+    unless ``distinct_gpus`` is off (the one-GPU --share-gpu rehearsal), no two
+    ranks share a PCI bus id (one process per GPU)."""
+    if len(infos) != world:
+        raise RuntimeError(f"{len(infos)} rank records for a world of {world}")
+    for r, inf in enumerate(infos):
+        if inf["nranks"] != world or inf["rank"] != r:
+            raise RuntimeError(f"rank {r}: context created as rank {inf['rank']} of {inf['nranks']}")
+        if exchange == "rccl" and (inf["rccl_nranks"] != world or inf["rccl_rank"] != r):
+            raise RuntimeError(f"rank {r}: RCCL communicator reports rank {inf['rccl_rank']} of "
+                               f"{inf['rccl_nranks']}, the job has {world}")
+    buses = [inf["bus_id"] for inf in infos]
+    if distinct_gpus and len(set(buses)) != len(buses):
+        raise RuntimeError(f"ranks share a GPU: PCI bus ids {buses}")
+
+
 def comm_unique_id() -> bytes:
     buf = (ctypes.c_uint8 * 128)()
     check(load().spx_comm_unique_id(buf))
@@ -193,6 +213,18 @@ class Context:
     def attach_comm(self, uid: bytes):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(self._L.spx_attach_comm(self._h, buf))
+
+    def comm_info(self):
+        """What joined the exchange (spx_comm_info): the RCCL communicator's
+        own rank count, rank and device (-1 without one), this context's HIP
+        device ordinal and PCI bus id, and whether loop passes replay captured
+        hipGraphs (``graph``) or fell back to eager after a refused capture."""
+        out = (ctypes.c_int32 * 8)()
+        bus = ctypes.create_string_buffer(64)
+        check(self._L.spx_comm_info(self._h, out, bus))
+        return {"rccl_nranks": out[0], "rccl_rank": out[1], "rccl_device": out[2], "device": out[3],
+                "graph": bool(out[4]), "graph_fallback": bool(out[5]), "nranks": out[6], "rank": out[7],
+                "bus_id": bus.value.decode(errors="replace")}
 
     def mbox_export(self) -> bytes:
         """This rank's mailbox handle (spx_mbox_export): gather every rank's

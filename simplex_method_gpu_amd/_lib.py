@@ -49,6 +49,7 @@ SIGNATURES = {
     "spx_destroy": (None, [_p]),
     "spx_comm_unique_id": (ctypes.c_int, [_p]),
     "spx_attach_comm": (ctypes.c_int, [_p, _p]),
+    "spx_comm_info": (ctypes.c_int, [_p, _p, _p]),
     "spx_mbox_export": (ctypes.c_int, [_p, _p]),
     "spx_ftran_cols": (ctypes.c_int, [_p, _p]),
     "spx_mbox_attach": (ctypes.c_int, [_p, _p]),

@@ -788,6 +788,7 @@ int iterate(spx_ctx* x, int64_t k) {
 int iterate_persist(spx_ctx* x, int64_t k) {
     const int64_t target = x->pivots + k;
     int64_t left = k;
+    int32_t launches = 0;
     while (left > 0) {
         const bool fold = fold_due(x);
         if (fold) {
@@ -805,6 +806,7 @@ int iterate_persist(spx_ctx* x, int64_t k) {
         LoopArgs a = x->la;
         a.npasses = (int32_t)np;
         a.epoch = ++x->loop_epoch & 0x1ffffffu;  // 25 bits: the tag keeps 7 for pass and phase
+        a.call_launch = launches++;
         if (!x->timing) a.clock = nullptr;
         HIP_TRY(hipMemsetAsync(a.ls, 0, LOOP_STATE_RESET, x->stream));
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1182,6 +1184,29 @@ int spx_attach_comm(spx_ctx* x, const uint8_t id[SPX_COMM_ID_BYTES]) {
     HIP_TRY(hipSetDevice(x->device));
     NCCL_TRY(ncclCommInitRank(&x->comm, x->opts.nranks, u, x->opts.rank));
     x->comm_ready = true;
+    return SPX_OK;
+}
+
+int spx_comm_info(spx_ctx* x, int32_t out[SPX_COMM_INFO_FIELDS], char bus_id[SPX_BUS_ID_BYTES]) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    int cnt = -1, urank = -1, cdev = -1;
+    if (x->comm_ready) {
+        NCCL_TRY(ncclCommCount(x->comm, &cnt));
+        NCCL_TRY(ncclCommUserRank(x->comm, &urank));
+        NCCL_TRY(ncclCommCuDevice(x->comm, &cdev));
+    }
+    out[0] = cnt;
+    out[1] = urank;
+    out[2] = cdev;
+    out[3] = x->device;
+    out[4] = (x->graph_exec != nullptr && x->batch > 0) ? 1 : 0;
+    out[5] = x->graph_fallback ? 1 : 0;
+    out[6] = x->opts.nranks;
+    out[7] = x->opts.rank;
+    if (bus_id) {
+        std::memset(bus_id, 0, SPX_BUS_ID_BYTES);
+        HIP_TRY(hipDeviceGetPCIBusId(bus_id, SPX_BUS_ID_BYTES - 1, x->device));
+    }
     return SPX_OK;
 }
 

@@ -17,34 +17,49 @@ namespace spx {
 // err = 2, nores += 1 and every workgroup leaves at once -- those not yet
 // resident leave when they start, seeing err -- so the launch changes nothing
 // and the host reruns its passes as two-kernel passes (iterate_persist).
+// The failure is sticky: nores is not reset between the launches of one call,
+// so once a launch has found its grid not resident every later launch of that
+// call leaves at entry as well, and the device window stays where the host's
+// readback after the call finds it (a later resident launch could otherwise
+// start from a window the host had already counted as advanced).
+//
+// Timeout and completion are exclusive through the arrive word itself: a
+// workgroup that times out CASes arrive from the count it observed (< G) to
+// that count | ARRIVE_CLOSED.  A fetch_add that returns a value with the bit
+// set came after the close and leaves; a failed CAS means another workgroup
+// arrived (or closed) in between, so the spinner re-reads instead of closing.
+// Nobody proceeds unless it saw arrive == G with the bit clear, and once the
+// bit is set arrive can never read G.
 #ifndef SPX_ARRIVE_TICKS
 #define SPX_ARRIVE_TICKS 200000ull  // 2 ms
 #endif
+constexpr uint32_t ARRIVE_CLOSED = 0x80000000u;
 __device__ __forceinline__ bool grid_arrive(LoopState* ls, int* s_ok) {
     if (threadIdx.x == 0) {
         int ok = 1;
         const uint32_t G = gridDim.x;
         const uint32_t old = __hip_atomic_fetch_add(&ls->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ld_agent(&ls->err)) ok = 0;
+        if ((old & ARRIVE_CLOSED) || ld_agent(&ls->nores) || ld_agent(&ls->err)) ok = 0;
         else if (old + 1 < G) {
             const unsigned long long t0 = rtime();
             uint32_t spins = 0;
-            while (ld_agent(&ls->arrive) < G) {
-                if ((++spins & 63u) == 0) {
-                    if (ld_agent(&ls->err)) { ok = 0; break; }
-                    if (rtime() - t0 > SPX_ARRIVE_TICKS) {
-                        int expected = 0;  // the first to time out counts the launch
-                        if (__hip_atomic_compare_exchange_strong(&ls->err, &expected, 2, __ATOMIC_RELAXED,
-                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                            __hip_atomic_fetch_add(&ls->nores, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                uint32_t v = ld_agent(&ls->arrive);
+                if (v & ARRIVE_CLOSED) { ok = 0; break; }
+                if (v >= G) break;
+                if ((++spins & 63u) == 0 && rtime() - t0 > SPX_ARRIVE_TICKS) {
+                    // close the entry at the count seen; losing the CAS means
+                    // the count moved (or someone closed it): look again
+                    if (__hip_atomic_compare_exchange_strong(&ls->arrive, &v, v | ARRIVE_CLOSED, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        st_agent(&ls->err, 2);
+                        __hip_atomic_fetch_add(&ls->nores, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         drain_vmem();
                         ok = 0;
                         break;
                     }
                 }
             }
-            // (all arrived: a late err from a timed-out peer still wins)
-            if (ok && ld_agent(&ls->err)) ok = 0;
         }
         *s_ok = ok;
     }

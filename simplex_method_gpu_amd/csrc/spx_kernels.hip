@@ -2080,7 +2080,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     // themselves delay this kernel's waits)
     unsigned long long* const slot = nullptr;
     unsigned long long* const wgt =
-        (P.stamps && tid == 0) ? P.stamps + STAMP_FTRAN + (Sv.iter & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x : nullptr;
+        (P.stamps && tid == 0 && blockIdx.x < 4096) ? P.stamps + STAMP_FTRAN + (Sv.iter & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x : nullptr;
     if (wgt) {
         wgt[0] = t_wg_entry;
         wgt[1] = rtime();

@@ -50,6 +50,7 @@ struct LoopArgs {
     uint32_t epoch;             // tableau loop: launch number (tags of the partial words)
     void* xp;                   // tableau loop: G tagged pricing partials (spx_tableau.hip)
     void* xu;                   // tableau loop: G tagged ratio-test partials
+    int32_t call_launch;        // host: launch number within one spx_iterate call (SPX_LOOP_OVERSUB=2)
 };
 
 struct LoopCfg {
@@ -68,9 +69,8 @@ struct LoopCfg {
 hipError_t loop_prepare(const Params& P, int cus, LoopCfg& c, bool want_bc = false);
 hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hipStream_t s);
 
-// the grid a persistent launch uses (SPX_LOOP_OVERSUB=1: twice it, for tests)
-int loop_grid_launched(int grid);
-// SPX_LOOP_COOP=1 (diagnostics): hipLaunchCooperativeKernel as in round 1
-bool loop_coop_launch();
+// the grid a persistent launch uses (tests: SPX_LOOP_OVERSUB=1 oversubscribes
+// every launch, =2 only the first launch of each spx_iterate call)
+int loop_grid_launched(int grid, int call_launch);
 
 }  // namespace spx

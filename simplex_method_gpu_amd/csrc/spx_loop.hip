@@ -274,7 +274,9 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
     const int64_t row1 = (row0 + rpw < m) ? row0 + rpw : m;
     const dbl2* srcB = reinterpret_cast<const dbl2*>(Bw);
 
-    for (int pass = 0; pass < La.npasses && it < limit; ++pass) {
+    // nw < KW bounds every pass as well (uniform across the grid): the window
+    // never overflows whatever npasses the host asked for
+    for (int pass = 0; pass < La.npasses && it < limit && nw < KW; ++pass) {
         const bool pend = nw > 0;
         const int tau = nw - 1;
         unsigned long long* clk = (La.clock && wg0 && tid == 0) ? La.clock + 3 * (int64_t)pass : nullptr;
@@ -692,26 +694,24 @@ hipError_t launch_loop(const Params& P, const LoopArgs& a, const LoopCfg& c, hip
     // a plain launch: the grid (one workgroup per CU, per_cu >= 1 checked in
     // loop_prepare) is co-resident without the cooperative launch's check,
     // and the grid barrier is our own (spx_grid.h), so no cooperative queue
-    // (MI355X_MICROARCH.md coop-launch: +15-19 us host wall per launch)
-    if (loop_coop_launch())
-        return hipLaunchCooperativeKernel(fn, dim3(c.grid), dim3(c.block), args, (unsigned)c.lds_bytes, s);
-    return hipLaunchKernel(fn, dim3(loop_grid_launched(c.grid)), dim3(c.block), args, (size_t)c.lds_bytes, s);
-}
-
-// SPX_LOOP_COOP=1 (diagnostics): the round-1 cooperative launch instead of the
-// plain one (tools/tab_exit_probe.py, the exit-time crash under rocprofv3)
-bool loop_coop_launch() {
-    const char* v = std::getenv("SPX_LOOP_COOP");
-    return v && v[0] == '1';
+    // (MI355X_MICROARCH.md coop-launch: +15-19 us host wall per launch).  The
+    // round-1 cooperative launch is gone for good: a process that had made one
+    // faulted in the HIP runtime's exit teardown under rocprofv3
+    // (profiles/r03_coop_exit_segv.txt), so no switch brings it back.
+    return hipLaunchKernel(fn, dim3(loop_grid_launched(c.grid, a.call_launch)), dim3(c.block), args,
+                           (size_t)c.lds_bytes, s);
 }
 
 // SPX_LOOP_OVERSUB=1 (tests): launch 4,096 more workgroups than the
 // co-resident grid -- more than any GPU holds at once (at most 32 waves per
 // CU) -- so the entry check (grid_arrive) must fail and the host fall back to
-// two-kernel passes
-int loop_grid_launched(int grid) {
+// two-kernel passes.  SPX_LOOP_OVERSUB=2: only the first launch of a call, so
+// the later launches of that call would have a resident grid (the sticky
+// failure of grid_arrive must still send them home).
+int loop_grid_launched(int grid, int call_launch) {
     const char* v = std::getenv("SPX_LOOP_OVERSUB");
-    return (v && v[0] == '1') ? grid + 4096 : grid;
+    const bool over = v && (v[0] == '1' || (v[0] == '2' && call_launch == 0));
+    return over ? grid + 4096 : grid;
 }
 
 }  // namespace spx

@@ -1116,10 +1116,7 @@ hipError_t launch_tab_loop(const Params& P, const LoopArgs& a, const LoopCfg& c,
     void* args[] = {const_cast<Params*>(&P), const_cast<LoopArgs*>(&a), &cpw, &rw};
     // plain launch of a co-resident grid (c.grid <= CUs, per_cu >= 1): the
     // barriers and hand-offs are our own, see launch_loop
-    if (loop_coop_launch())
-        return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(c.grid),
-                                          dim3(c.block), args, (unsigned)c.lds_bytes, s);
-    return hipLaunchKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(loop_grid_launched(c.grid)),
+    return hipLaunchKernel(reinterpret_cast<const void*>(&k_tab_loop<TAB_BLOCK>), dim3(loop_grid_launched(c.grid, a.call_launch)),
                            dim3(c.block), args, (size_t)c.lds_bytes, s);
 }
 

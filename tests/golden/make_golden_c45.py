@@ -10,7 +10,12 @@ folds on the GPU's default path) and records:
   - z = c_B . x_b.
 Data only, written to ``tests/golden/oracle_c{4,5}_k130.npz``.
 
-    python tests/golden/make_golden_c45.py [C4|C5 ...]
+C3SE: the headline config (m=4096, n=16384, seed 0) with exact steepest-edge
+pricing (the oracle's se_choose, Goldfarb-Reid recurrence; README.md:16-17),
+the same K = 130 pivots, plus the pricing weights gamma_j after them ->
+``tests/golden/oracle_c3se_k130.npz``.
+
+    python tests/golden/make_golden_c45.py [C4|C5|C3SE ...]
 """
 from __future__ import annotations
 
@@ -24,7 +29,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import oracle  # noqa: E402
 
-CONFIGS = {"C4": (4096, 131072, 0), "C5": (16384, 65536, 0)}
+CONFIGS = {"C4": (4096, 131072, 0), "C5": (16384, 65536, 0), "C3SE": (4096, 16384, 0)}
+PRICING = {"C3SE": 2}  # oracle.solve(pricing=...): 2 = steepest edge
 K = 130
 
 
@@ -33,13 +39,15 @@ def make(name: str) -> str:
     t0 = time.time()
     A, b, c = oracle.generate(m, n, seed)
     t1 = time.time()
-    r = oracle.solve(A, b, c, max_iter=K, eps=1e-7, trace_cap=K, want_state=True)
+    pricing = PRICING.get(name, 0)
+    r = oracle.solve(A, b, c, max_iter=K, eps=1e-7, trace_cap=K, want_state=True, pricing=pricing)
     t2 = time.time()
     assert r.status == oracle.MAX_ITER and r.pivots == K, (r.status, r.pivots)
     out = os.path.join(HERE, f"oracle_{name.lower()}_k{K}.npz")
     np.savez(out, m=m, n=n, seed=seed, k=K, eps=1e-7, z=r.z,
              trace_p=r.trace_p.astype(np.int64), trace_q=r.trace_q.astype(np.int64),
-             b_ixs=r.b_ixs.astype(np.int64), x_b=r.x_b, y=r.y)
+             b_ixs=r.b_ixs.astype(np.int64), x_b=r.x_b, y=r.y, pricing=pricing,
+             **({"weights": r.weights} if pricing else {}))
     print(f"{name}: m={m} n={n} K={K} z={r.z:.15g} generate {t1 - t0:.1f} s, "
           f"oracle {t2 - t1:.1f} s -> {os.path.basename(out)}", flush=True)
     del A, r

@@ -54,7 +54,7 @@ def test_status_strings(spx):
     L = spx._lib.load()
     assert L.spx_status_string(0) == b"MAX_ITER exceeded."
     assert L.spx_status_string(2) == b"Problem unbounded."
-    assert L.spx_abi_version() == 5
+    assert L.spx_abi_version() == 6
 
 
 def _has_gpu():
@@ -112,3 +112,31 @@ def test_read_lp_ignores_trailing_text(spx, tmp_path):
     p.write_text("2 4\n1 1 1 0\n2 1 0 1\n4 5\n3 2 0 0\n\nExplanation: prose here\nOptimum: 9\n")
     m, n, A, b, c = spx.read_lp(str(p))
     assert (m, n) == (2, 4) and list(c) == [3, 2, 0, 0] and A.shape == (4, 2) and list(A[0]) == [1, 2]
+
+
+def _info(r, G, bus, rccl=True):
+    return {"rccl_nranks": G if rccl else -1, "rccl_rank": r if rccl else -1, "rccl_device": r, "device": r,
+            "graph": True, "graph_fallback": False, "nranks": G, "rank": r, "bus_id": bus}
+
+
+def test_check_ranks_rules(spx):
+    """bench.py's multi-GPU evidence check (spx.check_ranks over the ranks'
+    all-gathered spx_comm_info): RCCL must report the job's world size and
+    each rank's own rank, and no two ranks may sit on one PCI bus id."""
+    G = 8
+    good = [_info(r, G, f"0000:{0x11 + r:02x}:00.0") for r in range(G)]
+    spx.check_ranks(good, G)
+    with pytest.raises(RuntimeError, match="RCCL communicator reports"):
+        spx.check_ranks([dict(i, rccl_nranks=1) for i in good], G)
+    with pytest.raises(RuntimeError, match="RCCL communicator reports"):
+        spx.check_ranks(good[:1] + [dict(good[1], rccl_rank=0)] + good[2:], G)
+    with pytest.raises(RuntimeError, match="share a GPU"):
+        spx.check_ranks(good[:7] + [dict(good[7], bus_id=good[0]["bus_id"])], G)
+    with pytest.raises(RuntimeError, match="rank records"):
+        spx.check_ranks(good[:4], G)
+    with pytest.raises(RuntimeError, match="created as rank"):
+        spx.check_ranks([dict(i, nranks=4) for i in good], G)
+    mbox = [_info(r, 2, "0000:11:00.0", rccl=False) for r in range(2)]  # --share-gpu rehearsal
+    spx.check_ranks(mbox, 2, exchange="mbox", distinct_gpus=False)
+    with pytest.raises(RuntimeError, match="share a GPU"):
+        spx.check_ranks(mbox, 2, exchange="mbox")

@@ -11,11 +11,11 @@ oracle needs minutes and 11 GB of host memory at C5, too much for a GPU test).
 (k_fold, the compact-operand compaction k_bc_list / k_bc_gather) twice and
 its third window on the folded state:
   - C4 default: two-kernel window passes with the compact FTRAN operand;
-  - C4 as an in-process group of 8 column shards (B^-1 replicated, MINLOC
-    merge; the north-star partitioning, SURVEY.md §8e);
+  - C4 as in-process groups of 2, 4 and 8 column shards (B^-1 replicated,
+    MINLOC merge; the north-star partitioning, SURVEY.md §8e);
   - C5 default: two-kernel passes (compact FTRAN, the base row read from L2);
     C5 on the persistent loop k_loop (opt-in; A_p gathered on the column list
-    into LDS); C5 as a 2-shard group (the default dispatch, two ranks).
+    into LDS); C5 as 2- and 8-shard groups (the default dispatch at G ranks).
 Tolerances (fp64): (p, q) identical for every pivot; the same
 basis order; x_b and y within 1e-9 (relative max-norm); z within 1e-9.
 """
@@ -101,8 +101,10 @@ def test_c4_default_matches_oracle(spx, c4):
     _single(spx, c4, expect_persistent=False)
 
 
-def test_c4_group8_matches_oracle(spx, c4):
-    _group(spx, c4, 8)
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_c4_group_matches_oracle(spx, c4, G):
+    """BASELINE.json configs[3]: C4 pricing column-sharded 2/4/8 ways."""
+    _group(spx, c4, G)
 
 
 def test_c5_default_matches_oracle(spx, c5):
@@ -113,5 +115,11 @@ def test_c5_persistent_matches_oracle(spx, c5):
     _single(spx, c5, expect_persistent=True, persist=True)
 
 
-def test_c5_group2_matches_oracle(spx, c5):
-    _group(spx, c5, 2)
+@pytest.mark.parametrize("G", [2, 8])
+def test_c5_group_matches_oracle(spx, c5, G):
+    """BASELINE.json configs[4]: C5, 1 GPU vs 8-GPU sharded pricing.  At G = 8
+    each shard prices ~6,144 structural columns (plus 2,048 slacks) behind the
+    replicated compact FTRAN and fold -- the geometry the SCALE line times.
+    Eight contexts with replicated A (8.6 GB each) and B_w / compact operand
+    (2.1 GB each) hold ~105 GB of the 288 GB HBM."""
+    _group(spx, c5, G)

@@ -63,3 +63,37 @@ def test_comm1_row_shard_matches_single_rank(spx, oracle, graph_batch):
     o = oracle.solve(A, b, c, eps=1e-7)
     assert r.status == spx.SolveStatus.OptimumFound and r.pivots == o.pivots
     assert abs(r.z - o.z) <= 1e-9 * abs(o.z)
+
+
+def test_comm_info_one_rank(spx):
+    """spx_comm_info on a one-rank communicator: RCCL itself reports 1 rank,
+    rank 0, bound to the context's device; the bus id is the device's; the
+    captured graphs hold the all-gathers (or report the eager fallback).
+    check_ranks accepts it, and refuses a record claiming another world."""
+    with spx.Context(m=256, n=1024, seed=0, window=-1, comm1=True) as ctx:
+        before = ctx.comm_info()
+        ctx.attach_comm(spx.comm_unique_id())
+        ctx.iterate(40)
+        inf = ctx.comm_info()
+        cfg = ctx.config()
+    assert before["rccl_nranks"] == -1 and before["rccl_rank"] == -1
+    assert inf["rccl_nranks"] == 1 and inf["rccl_rank"] == 0
+    assert inf["rccl_device"] == inf["device"] >= 0
+    assert len(inf["bus_id"]) >= 7 and ":" in inf["bus_id"]
+    assert inf["graph"] == (cfg["graph_batch"] > 0) and inf["graph"] != inf["graph_fallback"]
+    print(f"comm_info: {inf}")
+    spx.check_ranks([inf], 1)
+    with pytest.raises(RuntimeError):
+        spx.check_ranks([inf], 2)
+    with pytest.raises(RuntimeError):
+        spx.check_ranks([inf, dict(inf, rank=1)], 2, exchange="mbox")  # same bus id twice
+
+
+def test_comm_info_single_rank_context(spx):
+    """Without a communicator: -1 for the RCCL fields, the device's bus id,
+    graph replay for the default dispatch."""
+    with spx.Context(m=256, n=1024, seed=0, window=-1) as ctx:
+        ctx.iterate(40)
+        inf = ctx.comm_info()
+    assert inf["rccl_nranks"] == -1 and inf["nranks"] == 1 and inf["graph"] and not inf["graph_fallback"]
+    spx.check_ranks([inf], 1, exchange="none")

@@ -125,3 +125,29 @@ def test_loop_not_coresident_falls_back(spx, oracle, monkeypatch, tableau):
     assert r.status == spx.SolveStatus.OptimumFound and r.pivots == ref.pivots
     assert list(tp) == list(ref.trace_p) and list(tq) == list(ref.trace_q)
     assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)
+
+
+@pytest.mark.parametrize("tableau", [False, True], ids=["k_loop", "k_tab_loop"])
+def test_loop_first_launch_not_coresident_mid_window(spx, oracle, monkeypatch, tableau):
+    """only the FIRST persistent launch of a call is not resident
+    (SPX_LOOP_OVERSUB=2), and the call starts mid-window.  The later launches
+    of that call would find a resident grid; the failure is sticky
+    (spx_grid.h grid_arrive reads LoopState::nores), so they leave at entry too
+    instead of running from a window the host already counted as advanced,
+    and the fallback makes every pivot of the call -- the oracle's pivots."""
+    m, n, seed = 300, 900, 3
+    A, b, c = oracle.generate(m, n, seed)
+    ref = oracle.solve(A, b, c, eps=1e-7, trace_cap=4096)
+    with spx.Context(A, b, c, eps=1e-7, window=16, persist=True, tableau=tableau, trace=4096) as ctx:
+        assert ctx.config()["persistent"] == 1
+        st, piv = ctx.iterate(6)  # resident: the window is now mid-way
+        assert piv == 6 and ctx.dispatch_stats()["persist_fallbacks"] == 0
+        monkeypatch.setenv("SPX_LOOP_OVERSUB", "2")
+        st, piv = ctx.iterate(60)  # 4+ launches; only the first is oversubscribed
+        assert piv == 66
+        assert ctx.dispatch_stats()["persist_fallbacks"] == 1
+        r = ctx.solve()
+        tp, tq = ctx.trace()
+    assert r.status == spx.SolveStatus.OptimumFound and r.pivots == ref.pivots
+    assert list(tp) == list(ref.trace_p) and list(tq) == list(ref.trace_q)
+    assert abs(r.z - ref.z) <= 1e-9 * abs(ref.z)

@@ -127,3 +127,54 @@ def test_steepest_large_m_global_v(spx, oracle):
         ctx.iterate(k)
         tp, tq = ctx.trace()
     assert list(tp) == list(ref.trace_p) and list(tq) == list(ref.trace_q)
+
+
+def test_steepest_c3_matches_oracle_fixture(spx):
+    """The headline config (C3: m=4096, n=16384, seed 0) with steepest edge:
+    the oracle's first 130 pivots (two eta-window folds; the committed
+    fixture tests/golden/oracle_c3se_k130.npz from make_golden_c45.py C3SE),
+    x_b / y / z within 1e-9, and after one more pricing pass the weights of
+    every non-basic column within 1e-9 (relative) of the oracle's."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = np.load(os.path.join(root, "tests", "golden", "oracle_c3se_k130.npz"))
+    K = int(g["k"])
+    m, n, seed = int(g["m"]), int(g["n"]), int(g["seed"])
+    assert (m, n, seed, int(g["pricing"])) == (4096, 16384, 0, STEEP)
+    with spx.Context(m=m, n=n, seed=seed, eps=float(g["eps"]), pricing=STEEP, trace=K) as ctx:
+        cfg = ctx.config()
+        assert cfg["window"] == 64 and cfg["persistent"] == 0
+        st, piv = ctx.iterate(K)
+        assert st == spx.SolveStatus.MaxIter and piv == K
+        tp, tq = ctx.trace()
+        s = ctx.state()
+        z = ctx.objective()
+        ctx.price()
+        w = ctx.weights()
+    assert np.array_equal(tp, g["trace_p"]), int(np.argmax(tp != g["trace_p"]))
+    assert np.array_equal(tq, g["trace_q"]), int(np.argmax(tq != g["trace_q"]))
+    assert np.array_equal(s["b_ixs"], g["b_ixs"])
+    for key in ("x_b", "y"):
+        ref = g[key]
+        assert np.max(np.abs(s[key] - ref)) <= 1e-9 * max(1.0, float(np.max(np.abs(ref)))), key
+    assert abs(z - float(g["z"])) <= 1e-9 * abs(float(g["z"]))
+    nb = _nonbasic(n, s["b_ixs"])
+    wr = g["weights"]
+    assert np.max(np.abs(w[nb] - wr[nb]) / wr[nb]) <= 1e-9
+
+
+def test_steepest_c3_solves_to_highs_optimum(spx):
+    """C3 solved to optimality with steepest edge: the HiGHS optimum and basis
+    set of the committed fixture (tests/golden/highs_c3.json), in fewer pivots
+    than Dantzig's 18,291 (the oracle's C3 trace)."""
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "tests", "golden", "highs_c3.json")) as f:
+        h = json.load(f)
+    with spx.Context(m=h["m"], n=h["n"], seed=h["seed"], eps=h["eps"], pricing=STEEP) as ctx:
+        r = ctx.solve()
+    print(f"C3 steepest edge: {r.pivots} pivots (Dantzig {h['oracle_pivots']})")
+    assert r.status == spx.SolveStatus.OptimumFound
+    assert abs(r.z - h["highs_z"]) <= 1e-9 * abs(h["highs_z"])
+    assert sorted(int(j) for j in r.b_ixs) == h["highs_basis"]
+    assert r.pivots < h["oracle_pivots"]
