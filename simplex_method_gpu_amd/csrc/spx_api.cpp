@@ -447,7 +447,12 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     if (ub == 1024 && rows == 8) rows = 4;  // <1024, 8> spills registers: not instantiated
     uc.block = ub;
     uc.rows = rows;
-    uc.bc_entry = !env_off("SPX_FTRAN_BC_ENTRY");
+    uc.bc_entry = env_off("SPX_FTRAN_BC_ENTRY") ? 0 : 1;
+    if (uc.bc_entry) {  // k_ftran_bc rows per wave (deferred tail; the same bits at every value)
+        const char* ev = std::getenv("SPX_FTRAN_RPW");
+        const int r = ev ? std::atoi(ev) : 0;
+        if (r == 1 || r == 2 || r == 4) uc.bc_entry = r;
+    }
     uc.mark = env_on("SPX_DIAG_MARK");
     const int64_t rows_per_wg = (int64_t)(ub / 64) * rows;
     uc.grid = (int)std::max<int64_t>(1, (P.mloc + rows_per_wg - 1) / rows_per_wg);

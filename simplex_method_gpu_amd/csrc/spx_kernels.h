@@ -19,7 +19,8 @@ struct UpdateCfg {
     int block;  // threads per workgroup (256 / 512 / 1024)
     int rows;   // B^-1 rows per wave (1/2/4/8)
     int grid;   // ceil(m / (block / 64 * rows))
-    int bc_entry;  // compact FTRAN, 1 row per wave: k_ftran_bc (1) or k_update<..., BC> (0)
+    int bc_entry;  // compact FTRAN, 1 row per wave: k_ftran_bc (>= 1) or k_update<..., BC> (0);
+                   // with the deferred tail, k_ftran_bc's rows per wave (1, 2, 4: SPX_FTRAN_RPW)
     int mark;      // diagnostic: k_mark before the launch (SPX_DIAG_MARK=1, stamps only)
 };
 

@@ -1953,20 +1953,39 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 // (launch bounds: 4 waves per SIMD, <= 128 VGPRs, so two 512-thread
 // workgroups share a CU and the C3 grid, 512 workgroups, is resident at once:
 // at 130 VGPRs it ran in two rounds, 11.6 -> 17.0 us)
-template <int BLOCK, bool DEFER>
-__global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
+//
+// RPW > 1 (deferred tail only; SPX_FTRAN_RPW): each wave takes RPW rows, so
+// a workgroup covers RPW of the one-row grid's slots -- slot g = blockIdx.x *
+// RPW + r holds rows g * WAVES + wave, exactly the rows the one-row grid's
+// workgroup g holds -- and publishes one partial per slot, merged over its
+// waves in the same order.  Every row's terms, every slot's partial and the
+// next pass's reduction over the slots are therefore those of RPW = 1, bit
+// for bit; what changes is that the per-workgroup work (the pricing
+// partials' reduction, A_p's gather on the list) is done by RPW times fewer
+// workgroups, each wave keeps RPW rows' loads in flight, and the grid fits
+// one workgroup per CU (<= 256 VGPRs).
+template <int BLOCK, bool DEFER, int RPW>
+__global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) {
+    static_assert(RPW == 1 || DEFER, "several rows per wave: the deferred-tail form only");
     DevState* st = P.st;
     using Lds = UpdLds<BLOCK>;
     constexpr int WAVES = BLOCK / 64;
     constexpr int NCH = BC_PF2;  // dbl2 chunks of the compact row requested at entry
+    // LDS: the RPW x WAVES wave partials, then A_p on the list
+    constexpr size_t RED_BYTES = RPW == 1 ? Lds::bytes : sizeof(UpdPartial) * WAVES * RPW + 16;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t m = P.m, L2 = P.L >> 1;
     const int KW = P.win;
-    const int64_t i = (int64_t)blockIdx.x * WAVES + wave;  // this wave's row
-    const bool rowv = i < m;
-    const int64_t ic = rowv ? i : m - 1;
+    int64_t irow[RPW], icl[RPW];
+    bool rowv[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        irow[r] = ((int64_t)blockIdx.x * RPW + r) * WAVES + wave;  // this wave's rows
+        rowv[r] = irow[r] < m;
+        icl[r] = rowv[r] ? irow[r] : m - 1;
+    }
     // ---- entry: everything independent of p (issue order = retire order)
     const int pgi = tid < P.price_grid ? tid : P.price_grid - 1;
     const PricePartial pwl = P.price_partials[pgi];
@@ -1976,11 +1995,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
         const int64_t c = tid + (int64_t)j * BLOCK;
         rlv[j] = P.rlist[c < m ? c : 0];
     }
-    const int32_t rmv = P.rmap[ic];
-    const double al0 = P.alpha0[ic], al1 = P.alpha1[ic];
-    const double cbv = P.c_B[ic], xb0 = P.x_b[ic];
-    const int64_t bix = P.b_ixs[ic];
-    const double urow = P.U[ic * KW + (lane < KW ? lane : 0)];
+    int32_t rmv[RPW];
+    double al0[RPW], al1[RPW], cbv[RPW], xb0[RPW], urow[RPW];
+    int64_t bix[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        rmv[r] = P.rmap[icl[r]];
+        al0[r] = P.alpha0[icl[r]];
+        al1[r] = P.alpha1[icl[r]];
+        cbv[r] = P.c_B[icl[r]];
+        xb0[r] = P.x_b[icl[r]];
+        bix[r] = P.b_ixs[icl[r]];
+        urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
+    }
     const double sxw_w = P.Wt[P.n * KW + (lane < KW ? lane : 0)];
     struct {
         int32_t status, nb_count, nw;
@@ -2000,14 +2027,18 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     // (the entry clock goes here: taken first, its kernel-argument test ahead
     // of the loads reordered them, 11.7 -> 13.0 us)
     const unsigned long long t_wg_entry = P.stamps ? rtime() : 0ull;
-    // the compact row's first NCH chunks (S and the state are scalars: one wait)
-    const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + ic * ldc);
-    dbl2 pf[NCH];
+    // the compact rows' first NCH chunks (S and the state are scalars: one wait)
+    const dbl2* brow[RPW];
+    dbl2 pf[RPW][NCH];
 #pragma unroll
-    for (int t = 0; t < NCH; ++t) {
-        const int k2 = lane + 64 * t;
-        const int kk = (t == 0) ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
-        pf[t] = brow[kk];
+    for (int r = 0; r < RPW; ++r) {
+        brow[r] = reinterpret_cast<const dbl2*>(P.bc + icl[r] * ldc);
+#pragma unroll
+        for (int t = 0; t < NCH; ++t) {
+            const int k2 = lane + 64 * t;
+            const int kk = (t == 0) ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
+            pf[r][t] = brow[r][kk];
+        }
     }
     const int64_t qp = Sv.q;
     const bool pend = Sv.nw > 0;
@@ -2080,7 +2111,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     // themselves delay this kernel's waits)
     unsigned long long* const slot = nullptr;
     unsigned long long* const wgt =
-        (P.stamps && tid == 0 && blockIdx.x < 4096) ? P.stamps + STAMP_FTRAN + (Sv.iter & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x : nullptr;
+        (P.stamps && tid == 0 && blockIdx.x < 4096) ? P.stamps + STAMP_FTRAN + (Sv.iter & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x
+                                                    : nullptr;
     if (wgt) {
         wgt[0] = t_wg_entry;
         wgt[1] = rtime();
@@ -2102,7 +2134,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     double apv[BC_RL];
 #pragma unroll
     for (int j = 0; j < BC_RL; ++j) apv[j] = (tid + j * BLOCK < Sbc) ? apd[rlv[j]] : 0.0;
-    const double auv = apd[ic];
+    double auv[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) auv[r] = apd[icl[r]];
     const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
                                    : P.Wt + p * KW;
     const double wlr = wrec[lane < KW ? lane : 0];
@@ -2129,16 +2163,20 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     double* a_new = par ? P.alpha0 : P.alpha1;
     const double aqp = Sv.aq;
     const bool upd_x = Sv.xb_applied < it;
-    const double ei = (pend && rowv) ? eta_entry(par ? al1 : al0, i, qp, aqp) : 0.0;
+    double ei[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) ei[r] = (pend && rowv[r]) ? eta_entry(par ? al1[r] : al0[r], irow[r], qp, aqp) : 0.0;
     unsigned long long* const win = nullptr;
     // ---- compact FTRAN (as k_update BC): the unit term first (lane 0), then
     // this lane's chunks lane + 64 t ascending, .x before .y; A_p gathered
     // onto the list in LDS blocks of BC_APC columns
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* apc = reinterpret_cast<double*>(smem + Lds::bytes);
+    double* apc = reinterpret_cast<double*>(smem + RED_BYTES);
     const dbl2* apc2 = reinterpret_cast<const dbl2*>(apc);
     const int S = Sbc;
-    double a = (rowv && lane == 0 && rmv < 0) ? auv : 0.0;
+    double a[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) a[r] = (rowv[r] && lane == 0 && rmv[r] < 0) ? auv[r] : 0.0;
     for (int cb = 0; cb < S || cb == 0; cb += BC_APC) {
         const int ce = S < cb + BC_APC ? S : cb + BC_APC;
         if (cb > 0) lds_barrier();  // the previous block's reads are done
@@ -2151,30 +2189,33 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
         lds_barrier();
         if (wgt && cb == 0) wgt[2] = rtime();
         const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
-        if (rowv) {
-            auto take = [&](dbl2 v, int k2) {
-                const dbl2 w = apc2[k2 - kb];
-                if (2 * k2 < S) a = fma(v.x, w.x, a);
-                if (2 * k2 + 1 < S) a = fma(v.y, w.y, a);
-            };
-            if (cb == 0) {
 #pragma unroll
-                for (int t = 0; t < NCH; ++t) {
-                    const int k2 = lane + 64 * t;
-                    if (k2 < ke) take(pf[t], k2);
+        for (int r = 0; r < RPW; ++r) {
+            if (rowv[r]) {
+                auto take = [&](dbl2 v, int k2) {
+                    const dbl2 w = apc2[k2 - kb];
+                    if (2 * k2 < S) a[r] = fma(v.x, w.x, a[r]);
+                    if (2 * k2 + 1 < S) a[r] = fma(v.y, w.y, a[r]);
+                };
+                if (cb == 0) {
+#pragma unroll
+                    for (int t = 0; t < NCH; ++t) {
+                        const int k2 = lane + 64 * t;
+                        if (k2 < ke) take(pf[r][t], k2);
+                    }
                 }
-            }
-            for (int k0 = (cb == 0 ? NCH * 64 : kb); k0 < ke; k0 += 8 * 64) {
-                dbl2 v[8];
+                for (int k0 = (cb == 0 ? NCH * 64 : kb); k0 < ke; k0 += 8 * 64) {
+                    dbl2 v[8];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int k2 = k0 + lane + 64 * t;
-                    v[t] = brow[k2 < ke ? k2 : kb];
-                }
+                    for (int t = 0; t < 8; ++t) {
+                        const int k2 = k0 + lane + 64 * t;
+                        v[t] = brow[r][k2 < ke ? k2 : kb];
+                    }
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int k2 = k0 + lane + 64 * t;
-                    if (k2 < ke) take(v[t], k2);
+                    for (int t = 0; t < 8; ++t) {
+                        const int k2 = k0 + lane + 64 * t;
+                        if (k2 < ke) take(v[t], k2);
+                    }
                 }
             }
         }
@@ -2184,41 +2225,64 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     // issued before the merge put their write acknowledgements on the path
     // to the publish)
     const double wl = lane < Sv.nw ? wlr : 0.0;
-    double acc = 0.0;
-    if (rowv) {
-        const double cu = lane < tau ? urow : (lane == tau ? ei : 0.0);
-        acc = fma(cu, wl, a);
+    double acc[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        acc[r] = 0.0;
+        if (rowv[r]) {
+            const double cu = lane < tau ? urow[r] : (lane == tau ? ei[r] : 0.0);
+            acc[r] = fma(cu, wl, a[r]);
+        }
     }
     double sxw = 0.0;
     if (pend) sxw = sx_x + wave_sum(lane < tau ? mul_nc(sxw_u, sxw_w) : 0.0);
     const double s_x = upd_x ? sxw : 0.0;
 
-    // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partial
-    UpdPartial wp = upd_empty();
-    double al = 0.0, xb = xb0;
-    if (rowv) {
-        al = wave_sum(acc);
-        if (upd_x) xb = fma(s_x, ei, xb);
-        const bool pos = al > P.piv_tol;
-        const double th = ratio_key(P, xb, al);
-        wp.nonpos += !pos;
-        wp.T = fma(cbv, al, wp.T);
-        if (argmin_better(th, i, wp.theta, wp.idx)) {
-            wp.theta = th;
-            wp.idx = i;
-            wp.a_w = al;
-            wp.cb_w = cbv;
-            wp.bix_w = bix;
+    // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partials
+    // (the RPW rows' butterflies interleaved: each value's own bits)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        double t[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) t[r] = __shfl_xor(acc[r], off, 64);
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) acc[r] += t[r];
+    }
+    UpdPartial wp[RPW];
+    double al[RPW], xb[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        wp[r] = upd_empty();
+        al[r] = 0.0;
+        xb[r] = xb0[r];
+        if (rowv[r]) {
+            al[r] = acc[r];
+            if (upd_x) xb[r] = fma(s_x, ei[r], xb[r]);
+            const bool pos = al[r] > P.piv_tol;
+            const double th = ratio_key(P, xb[r], al[r]);
+            wp[r].nonpos += !pos;
+            wp[r].T = fma(cbv[r], al[r], wp[r].T);
+            if (argmin_better(th, irow[r], wp[r].theta, wp[r].idx)) {
+                wp[r].theta = th;
+                wp[r].idx = irow[r];
+                wp[r].a_w = al[r];
+                wp[r].cb_w = cbv[r];
+                wp[r].bix_w = bix[r];
+            }
         }
     }
     // alpha_i (read back by the next pass / k_flush), x_b, the pending eta
     // entry into U, and the basic columns' Wt entries (s_x in Wt[n])
     auto store_row = [&]() {
-        if (rowv && lane == 0) {
-            if (pend) P.U[i * KW + tau] = ei;
-            a_new[i] = al;
-            if (upd_x) P.x_b[i] = xb;
-            if (pend) P.Wt[bix * KW + tau] = (i == qp) ? aqp : 0.0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            if (rowv[r] && lane == 0) {
+                const int64_t i = irow[r];
+                if (pend) P.U[i * KW + tau] = ei[r];
+                a_new[i] = al[r];
+                if (upd_x) P.x_b[i] = xb[r];
+                if (pend) P.Wt[bix[r] * KW + tau] = (i == qp) ? aqp : 0.0;
+            }
         }
         if (pend && blockIdx.x == 0 && tid == 0) P.Wt[P.n * KW + tau] = sxw;
     };
@@ -2227,7 +2291,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     if constexpr (!DEFER) store_row();
     UpdPartial* red = reinterpret_cast<UpdPartial*>(smem + Lds::red);
     int* s_last = reinterpret_cast<int*>(smem + Lds::last);
-    if (lane == 0) red[wave] = wp;
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) red[r * WAVES + wave] = wp[r];
+    }
     lds_barrier();
     if (P.split_tail) {  // k_tail merges after the kernel boundary
         if (tid == 0) {
@@ -2238,23 +2305,25 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
         return;
     }
     if constexpr (DEFER) {  // the next pricing pass (or k_apply_tail) reduces the partials
-        if (tid == 0) {
-            UpdPartial w = red[0];
-            for (int k = 1; k < WAVES; ++k) upd_merge(w, red[k]);
-            upd_publish<true>(P, blockIdx.x, w);
+        if (tid < RPW) {
+            const int r = tid;
+            const int g = blockIdx.x * RPW + r;
+            UpdPartial w = red[r * WAVES];
+            for (int k = 1; k < WAVES; ++k) upd_merge(w, red[r * WAVES + k]);
+            if (g < P.tail_parts) upd_publish<true>(P, g, w);
             if (wgt) wgt[3] = rtime();
-            if (blockIdx.x == 0) {
-                TailRec* r = P.trec;
-                r->it = it;
-                r->p = p;
-                r->e_rep = !P.devex ? min_e : (P.defer_price ? e_enter : *P.dvx_e);
-                r->c_p = rc_p;
-                r->wp = rwp;
-                r->cnt = Sv.nb_count;
-                r->kp = rkp;
-                r->last = rlast;
-                r->nw = Sv.nw;
-                r->fresh = 1;
+            if (g == 0) {
+                TailRec* rec = P.trec;
+                rec->it = it;
+                rec->p = p;
+                rec->e_rep = !P.devex ? min_e : (P.defer_price ? e_enter : *P.dvx_e);
+                rec->c_p = rc_p;
+                rec->wp = rwp;
+                rec->cnt = Sv.nb_count;
+                rec->kp = rkp;
+                rec->last = rlast;
+                rec->nw = Sv.nw;
+                rec->fresh = 1;
             }
         }
         store_row();
@@ -2288,7 +2357,6 @@ __global__ __launch_bounds__(BLOCK, 4) void k_ftran_bc(Params P) {
     update_tail<BLOCK>(P, st, p, min_e, it, smem, gridDim.x, &tpre);
     stamp_tail(slot, t_tail, win);
 }
-
 // Window tableau FTRAN (spx_tabdev.h): one lane per row,
 // alpha_i = T_w[i,p] + sum_s U[i][s] Wt[p][s] — no B_w stream — then the
 // pending eta column into U, the basic columns' Wt entries, x_b, the ratio
@@ -2923,38 +2991,47 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
     return hipGetLastError();
 }
 
-template <int BLOCK, bool DEFER>
+// grid: the one-row grid's workgroups (= partial slots); RPW rows per wave
+// take ceil(grid / RPW) workgroups
+template <int BLOCK, bool DEFER, int RPW>
 static hipError_t launch_ftran_bc_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    const size_t lds = UpdLds<BLOCK>::bytes + (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8;
+    const size_t red = RPW == 1 ? UpdLds<BLOCK>::bytes : sizeof(UpdPartial) * (BLOCK / 64) * RPW + 16;
+    const size_t lds = red + (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8;
+    const int g = (grid + RPW - 1) / RPW;
     if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK, DEFER>),
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK, DEFER, RPW>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         if (e != hipSuccess) return e;
     }
     if (e0 || e1)
-        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW>), dim3(g), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     else
-        hipLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW>), dim3(g), dim3(BLOCK), lds, s, P);
     return hipGetLastError();
 }
 
 // deferred ratio-test tail: its own instantiation (no tail code, and the
-// tail's registers stay out of the hand-off kernel)
+// tail's registers stay out of the hand-off kernel); rows per wave (the
+// deferred form only; bc_entry = SPX_FTRAN_RPW, UpdateCfg)
 template <int BLOCK>
-static hipError_t launch_ftran_bc(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    return P.defer_tail ? launch_ftran_bc_t<BLOCK, true>(P, grid, s, e0, e1)
-                        : launch_ftran_bc_t<BLOCK, false>(P, grid, s, e0, e1);
+static hipError_t launch_ftran_bc(const Params& P, int grid, int rpw, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (!P.defer_tail) return launch_ftran_bc_t<BLOCK, false, 1>(P, grid, s, e0, e1);
+    if constexpr (BLOCK == 512) {
+        if (rpw == 2) return launch_ftran_bc_t<BLOCK, true, 2>(P, grid, s, e0, e1);
+        if (rpw == 4) return launch_ftran_bc_t<BLOCK, true, 4>(P, grid, s, e0, e1);
+    }
+    return launch_ftran_bc_t<BLOCK, true, 1>(P, grid, s, e0, e1);
 }
 
 template <int BLOCK, int R>
-static hipError_t launch_update_t(const Params& P, int grid, bool bc_entry, hipStream_t s, hipEvent_t e0,
+static hipError_t launch_update_t(const Params& P, int grid, int bc_entry, hipStream_t s, hipEvent_t e0,
                                   hipEvent_t e1) {
     if (P.row_shard) return launch_update_k<BLOCK, R, true, false>(P, grid, s, e0, e1);
     if (!P.win) return launch_update_k<BLOCK, R, false, false>(P, grid, s, e0, e1);
     // B_w loads: default policy while B_w fits the Infinity Cache beside the
     // window state (spx_common.h SPX_NT_BWIN), non-temporal beyond
     if (P.bc) {  // compact FTRAN
-        if (R == 1 && bc_entry) return launch_ftran_bc<BLOCK>(P, grid, s, e0, e1);
+        if (R == 1 && bc_entry) return launch_ftran_bc<BLOCK>(P, grid, bc_entry, s, e0, e1);
         return launch_update_k<BLOCK, R, false, true, 0, true>(P, grid, s, e0, e1);
     }
     if (win_b_cached(P)) return launch_update_k<BLOCK, R, false, true, 0>(P, grid, s, e0, e1);
@@ -3119,11 +3196,11 @@ hipError_t launch_finalize_rs(const Params& P, hipStream_t s) {
 template <int BLOCK>
 static hipError_t launch_update_b(const Params& P, const UpdateCfg& c, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     switch (c.rows) {
-        case 1: return launch_update_t<BLOCK, 1>(P, c.grid, c.bc_entry != 0, s, e0, e1);
-        case 2: return launch_update_t<BLOCK, 2>(P, c.grid, c.bc_entry != 0, s, e0, e1);
-        case 4: return launch_update_t<BLOCK, 4>(P, c.grid, c.bc_entry != 0, s, e0, e1);
+        case 1: return launch_update_t<BLOCK, 1>(P, c.grid, c.bc_entry, s, e0, e1);
+        case 2: return launch_update_t<BLOCK, 2>(P, c.grid, c.bc_entry, s, e0, e1);
+        case 4: return launch_update_t<BLOCK, 4>(P, c.grid, c.bc_entry, s, e0, e1);
         case 8:
-            if constexpr (BLOCK <= 512) return launch_update_t<BLOCK, 8>(P, c.grid, c.bc_entry != 0, s, e0, e1);
+            if constexpr (BLOCK <= 512) return launch_update_t<BLOCK, 8>(P, c.grid, c.bc_entry, s, e0, e1);
             break;
     }
     return hipErrorInvalidValue;

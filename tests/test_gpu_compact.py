@@ -192,3 +192,24 @@ def test_compact_entry_kernel_same_bits(spx, kw):
     for key in ("b_ixs", "x_b", "y", "binv"):
         assert np.array_equal(a[1][key], b[1][key]), key
     assert a[3].pivots == b[3].pivots and a[3].z == b[3].z
+
+
+@pytest.mark.parametrize("rpw", [2, 4])
+@pytest.mark.parametrize("kw", [dict(m=2051, n=6000, seed=5, window=64), dict(m=4096, n=16384, seed=0),
+                                dict(m=2304, n=9000, seed=3, window=16)],
+                         ids=["m2051-w64", "C3", "m2304-w16"])
+def test_ftran_rows_per_wave_same_bits(spx, kw, rpw):
+    """k_ftran_bc with RPW rows per wave (SPX_FTRAN_RPW; the deferred tail's
+    form): each workgroup covers RPW of the one-row grid's partial slots with
+    the same rows and the same merges, so states, traces and optima are those
+    of one row per wave bit for bit -- including a last workgroup whose slots
+    run past the grid (m = 2051: 257 slots) and a sliver of a last wave."""
+    a = _run(spx, False, 200, persist=False, **kw)
+    with _env(SPX_FTRAN_RPW=str(rpw)):
+        with spx.Context(persist=False, **kw) as ctx:
+            assert ctx.config()["defer_tail"] == 1
+        b = _run(spx, False, 200, persist=False, **kw)
+    assert np.array_equal(a[2], b[2])
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    assert a[3].pivots == b[3].pivots and a[3].z == b[3].z

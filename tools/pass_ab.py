@@ -4,7 +4,8 @@ each: the A/B of whole passes (tools/ab_libs.py gives the event-timed kernel
 split).  Also used for timing-only builds whose pivots do not advance (one
 graph launch still runs 63 passes).
     python tools/pass_ab.py default simplex_method_gpu_amd/_build/xNAME/libsimplex.so ...
-    SPX_DEFER_TAIL=0 python tools/pass_ab.py default   # env knobs apply to every build"""
+    SPX_DEFER_TAIL=0 python tools/pass_ab.py default   # env knobs apply to every build
+    python tools/pass_ab.py env:SPX_FTRAN_RPW=1 env:SPX_FTRAN_RPW=4   # knobs per entry"""
 import json
 import os
 import subprocess
@@ -29,7 +30,11 @@ res = {l: [] for l in libs}
 for r in range(3):
     for l in libs:
         env = dict(os.environ)
-        if l != "default":
+        if l.startswith("env:"):  # env:VAR=VAL[,VAR=VAL]: the default build with these knobs
+            for kv in l[4:].split(","):
+                k, v = kv.split("=", 1)
+                env[k] = v
+        elif l != "default":
             env["SPX_LIB"] = os.path.join(ROOT, l)
         out = subprocess.run([sys.executable, "-c", CHILD], capture_output=True, text=True, env=env, timeout=200)
         line = [x for x in out.stdout.splitlines() if x.startswith("{")]

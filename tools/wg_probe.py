@@ -41,6 +41,7 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
         lo, hi = (0, 1) if w[0]["price"][:, 0].min() < w[1]["price"][:, 0].min() else (1, 0)
         A, B = w[lo], w[hi]
         pa, fa, pb = (A["price"].astype(np.int64), A["ftran"].astype(np.int64), B["price"].astype(np.int64))
+        fa = fa[fa[:, 0] > 0]  # (SPX_FTRAN_RPW > 1: fewer workgroups than partial slots)
         p0 = pa[:, 0].min()
         f0 = fa[:, 0].min()
         put("price_entry_spread", pa[:, 0].max() - p0)
