@@ -582,7 +582,7 @@ int do_reset(spx_ctx* x) {
     if (x->P.bc) {  // B_w = I: no column list
         HIP_TRY(hipMemsetAsync(x->P.rleft, 0, (size_t)x->L * sizeof(int32_t), x->stream));
         HIP_TRY(hipMemsetAsync(x->P.rmap, 0xFF, (size_t)x->L * sizeof(int32_t), x->stream));
-        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, 4 * sizeof(int32_t), x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, BC_N_WORDS * sizeof(int32_t), x->stream));
     }
     SPX_TRY(tab_rebuild(x, true));
     HIP_TRY(hipStreamSynchronize(x->stream));
@@ -984,7 +984,7 @@ int reinvert_basis(spx_ctx* x, const int64_t* basis) {
         HIP_TRY(hipMemcpyAsync(x->P.rleft, left.data(), (size_t)x->L * sizeof(int32_t), hipMemcpyHostToDevice,
                                x->stream));
         HIP_TRY(hipMemsetAsync(x->P.rmap, 0xFF, (size_t)x->L * sizeof(int32_t), x->stream));
-        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, 4 * sizeof(int32_t), x->stream));
+        HIP_TRY(hipMemsetAsync(x->P.bc_n, 0, BC_N_WORDS * sizeof(int32_t), x->stream));
         HIP_TRY(launch_compact(x->P, x->stream));
         HIP_TRY(hipStreamSynchronize(x->stream));  // (left is a host buffer)
     }
@@ -1045,21 +1045,29 @@ int set_slack_flags(spx_ctx* x) {
     x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
     if (x->bc_want && ident) {  // compact FTRAN operand (do_reset initialises it)
         Params& P = x->P;
-        // m x L more doubles (2.1 GB at C5): when they do not fit, the dense
+        // 2 x m x L more doubles (2 x 2.1 GB at C5; the compact fold writes
+        // the other buffer, spx_device.h): when they do not fit, the dense
         // B_w stream that fit before is kept (every kernel tests P.bc)
-        void* d = nullptr;
-        if (hipMalloc(&d, (size_t)(m * x->L) * sizeof(double)) != hipSuccess) {
-            (void)hipGetLastError();
-            x->bc_want = false;
-            return SPX_OK;
+        void* d[2] = {nullptr, nullptr};
+        for (int k = 0; k < 2; ++k) {
+            if (hipMalloc(&d[k], (size_t)(m * x->L) * sizeof(double)) != hipSuccess) {
+                (void)hipGetLastError();
+                if (k == 1) (void)hipFree(d[0]);
+                x->bc_want = false;
+                return SPX_OK;
+            }
         }
-        x->allocs.push_back(d);
-        HIP_TRY(hipMemsetAsync(d, 0, (size_t)(m * x->L) * sizeof(double), x->stream));
-        P.bc = static_cast<double*>(d);
+        for (int k = 0; k < 2; ++k) {
+            x->allocs.push_back(d[k]);
+            HIP_TRY(hipMemsetAsync(d[k], 0, (size_t)(m * x->L) * sizeof(double), x->stream));
+        }
+        P.bc = static_cast<double*>(d[0]);
+        P.bc1 = static_cast<double*>(d[1]);
+        P.cfold = env_on("SPX_DENSE_FOLD") ? 0 : 1;
         SPX_TRY(x->alloc(&P.rlist, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rmap, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rleft, (size_t)x->L));
-        SPX_TRY(x->alloc(&P.bc_n, 4));
+        SPX_TRY(x->alloc(&P.bc_n, BC_N_WORDS));
     }
     // deferred ratio-test tail (TailRec, spx_device.h): compact FTRAN passes
     // (k_ftran_bc, one row per wave) with 512- or 256-thread pricing -- the

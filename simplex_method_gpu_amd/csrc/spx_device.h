@@ -315,12 +315,24 @@ struct Params {
     // (or, after a reinversion, when slack k is not basic in row k): a
     // superset of the non-unit columns; bc_n[0] = S, bc_n[1] = the row pitch.
     // nullptr: dense FTRAN.
+    // Two buffers of that shape: bc_n[2] selects the active one (bc or bc1).
+    // The compact fold (k_cfold) reads the active buffer at the old pitch,
+    // writes the folded rows at the new pitch into the other one, scatters
+    // the same values into the dense B_w and flips bc_n[2]; bc_n[3] / bc_n[4]
+    // hold S and the pitch before k_bc_list appended the window's rows.
     double* bc;
+    double* bc1;
+    int32_t cfold;  // the fold updates the listed columns only (k_cfold; SPX_DENSE_FOLD=1: k_fold + gather)
+    int32_t pad_bc;
     int32_t* rlist;
     int32_t* rmap;
     int32_t* rleft;
     int32_t* bc_n;
 };
+
+// the compact operand's active buffer (bc_n[2])
+__host__ __device__ inline double* bc_buf(const Params& P, int sel) { return sel ? P.bc1 : P.bc; }
+constexpr int BC_N_WORDS = 8;
 
 __device__ __forceinline__ void record_pivot(const Params& P, int64_t it, int64_t p, int64_t q) {
     if (P.trace && it < P.trace_cap) {

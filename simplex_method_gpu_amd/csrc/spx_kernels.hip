@@ -161,6 +161,7 @@ template <int BLOCK, bool PLAIN>
 __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red);
 template <bool PLAIN = false>
 __device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g);
+__device__ __forceinline__ UpdPartial wave_reduce_partial(const UpdPartial& w);
 // the deferred ratio-test tail's bookkeeping (TailRec; defined with the tail)
 __device__ __forceinline__ void apply_deferred_tail(const Params& P, DevState* st, const TailRec& R,
                                                     const UpdPartial& t);
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // its own staging loads: vmcnt retires in order)
     __shared__ TailRec s_rec;
     __shared__ UpdPartial s_tp;
-#ifdef SPX_DIAG_FETCH_STAMP
+#if defined(SPX_DIAG_FETCH_STAMP) || defined(SPX_DIAG_MERGE_STAMP)
     unsigned long long t_fetch_all = 0;
 #endif
     if (P.defer_tail) {
@@ -237,6 +238,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 t = reduce_partial_pair<BLOCK>(w0, w1, s_ured);
             } else {
                 for (int g = tid + BLOCK; g < P.tail_parts; g += BLOCK) upd_merge(w0, upd_fetch<true>(P, g));
+#ifdef SPX_DIAG_MERGE_STAMP  // timing probe: the wave reductions alone, then the merge (pw[3] / pw[2])
+                {
+                    const UpdPartial o = wave_reduce_partial(w0);
+                    asm volatile("" ::"v"(o.theta), "v"(o.T));
+                    t_fetch_all = rtime();
+                }
+#endif
                 t = reduce_partial_block<BLOCK, true>(w0, s_ured);
             }
             const int64_t q = t.idx;
@@ -747,7 +755,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         pw[0] = t_pw0;
         pw[1] = rtime();
         pw[2] = t_pw1;
-#ifdef SPX_DIAG_FETCH_STAMP
+#if defined(SPX_DIAG_FETCH_STAMP) || defined(SPX_DIAG_MERGE_STAMP)
         pw[3] = t_fetch_all;
 #else
         pw[3] = t_pw2;
@@ -1395,7 +1403,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         // the loads stay unconditional and the waits below exact)
         // (each row clamped on its own: in a partly filled last wave, row u <
         // nvalid must be row pf_row + u, which the compact path consumes)
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? P.bc : P.B0);
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(BC ? bc_buf(P, P.bc_n[2]) : P.B0);
         const int64_t ld2r = BC ? (int64_t)(P.bc_n[1] >> 1) : L2c;  // row pitch (compact: bc_pitch)
 #pragma unroll
         for (int t = 0; t < PFU; ++t) {
@@ -1517,7 +1525,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         Sbc = P.bc_n[0];
         const int64_t L2c = P.L >> 1;
         const int64_t ld2r = P.bc_n[1] >> 1;
-        const dbl2* b0 = reinterpret_cast<const dbl2*>(P.bc);
+        const dbl2* b0 = reinterpret_cast<const dbl2*>(bc_buf(P, P.bc_n[2]));
 #pragma unroll
         for (int t = BC_PF; t < BC_PF2; ++t) {
             const int k2 = lane + 64 * t;
@@ -2024,6 +2032,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     Sv.nw = st->nw;
     const int Sbc = P.bc_n[0];
     const int64_t ldc = P.bc_n[1];  // compact row pitch (k_bc_list)
+    const double* const bcb = bc_buf(P, P.bc_n[2]);  // the active buffer
     // (the entry clock goes here: taken first, its kernel-argument test ahead
     // of the loads reordered them, 11.7 -> 13.0 us)
     const unsigned long long t_wg_entry = P.stamps ? rtime() : 0ull;
@@ -2032,7 +2041,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     dbl2 pf[RPW][NCH];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-        brow[r] = reinterpret_cast<const dbl2*>(P.bc + icl[r] * ldc);
+        brow[r] = reinterpret_cast<const dbl2*>(bcb + icl[r] * ldc);
 #pragma unroll
         for (int t = 0; t < NCH; ++t) {
             const int k2 = lane + 64 * t;
@@ -3038,7 +3047,9 @@ static hipError_t launch_update_t(const Params& P, int grid, int bc_entry, hipSt
     return launch_update_k<BLOCK, R, false, true, 1>(P, grid, s, e0, e1);
 }
 
+hipError_t launch_cfold(const Params& P, int min_nw, int cus, hipStream_t s);
 hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
+    if (P.bc && P.cfold) return launch_cfold(P, min_nw, cus, s);  // the listed columns only
     if (P.tab) {  // T_w and dw first: k_fold resets the window
         const hipError_t e = launch_tab_fold(P, min_nw, cus, s);
         if (e != hipSuccess) return e;
@@ -3061,6 +3072,8 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s) {
     return launch_compact(P, s);  // the compact FTRAN operand follows B_w
 }
 
+
+
 hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
     hipLaunchKernelGGL(k_tail, dim3(1), dim3(1024), 0, s, P, nparts);
     return hipGetLastError();
@@ -3072,11 +3085,21 @@ hipError_t launch_tail(const Params& P, int nparts, hipStream_t s) {
 // order (k_bc_list, one workgroup), then every row of B_w is gathered onto
 // those columns (k_bc_gather).  The dense B_w stays the master copy.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_bc_list(Params P) {
+// min_nw > 0 (the compact fold): only when that fold runs (k_fold's test),
+// recording S and the pitch before the append in bc_n[3] / bc_n[4]
+__global__ __launch_bounds__(1024) void k_bc_list(Params P, int min_nw) {
     __shared__ int s_w[16];
     __shared__ int s_base;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_base = P.bc_n[0];
+    if (min_nw > 0) {
+        const int nw = P.st->nw;
+        if (nw < min_nw || nw < 2) return;
+    }
+    if (tid == 0) {
+        s_base = P.bc_n[0];
+        P.bc_n[3] = P.bc_n[0];
+        P.bc_n[4] = P.bc_n[1];
+    }
     __syncthreads();
     for (int64_t k0 = 0; k0 < P.m; k0 += 1024) {
         const int64_t k = k0 + tid;
@@ -3111,16 +3134,250 @@ constexpr int BC_ROWS = 4;  // rows per k_bc_gather workgroup
 __global__ __launch_bounds__(256) void k_bc_gather(Params P) {
     const int S = P.bc_n[0];
     const int64_t L = P.L, ldc = P.bc_n[1];
+    double* const bc = bc_buf(P, P.bc_n[2]);
     for (int r = 0; r < BC_ROWS; ++r) {
         const int64_t i = (int64_t)blockIdx.x * BC_ROWS + r;
         if (i >= P.m) break;
-        for (int c = threadIdx.x; c < S; c += 256) P.bc[i * ldc + c] = P.B0[i * L + P.rlist[c]];
+        for (int c = threadIdx.x; c < S; c += 256) bc[i * ldc + c] = P.B0[i * L + P.rlist[c]];
     }
 }
+// the whole operand from the dense B_w (reset, reinversion, warm start; and
+// after a dense fold, SPX_DENSE_FOLD=1)
 hipError_t launch_compact(const Params& P, hipStream_t s) {
     if (!P.bc) return hipSuccess;
-    hipLaunchKernelGGL(k_bc_list, dim3(1), dim3(1024), 0, s, P);
+    hipLaunchKernelGGL(k_bc_list, dim3(1), dim3(1024), 0, s, P, 0);
     hipLaunchKernelGGL(k_bc_gather, dim3((unsigned)((P.m + BC_ROWS - 1) / BC_ROWS)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Compact fold (Params::bc): the eta-window fold of k_fold
+// restricted to B_w's non-unit columns.  A column of B_w outside the list is
+// e_k and stays e_k (every r_t has an exact 0 there: B_w[q_t, k] = 0 for the
+// unit column k != q_t, and the window's leaving rows q_t join the list
+// first, k_bc_list), so only the m x S' listed entries change -- the dense
+// fold rewrites all m x L of them.  Per 64-column group of the new list:
+//   R: r_t = Qrows[t][k_c] + sum_{s<t} Urows[t][s] r_s (Qrows: the base rows
+//      k_price staged), by one wave, one lane per column, the s terms of each
+//      r_t in ascending order with the fold's zero coefficients -- the fma
+//      sequence of fold_rebuild_R4, so the bits of k_fold's R;
+//   tiles: the fold's MFMA tiles (fold_tile_take, v_mfma_f64_16x16x4f64, the
+//      same K order), rows read from the active buffer at the old pitch
+//      (columns the window added read as e_k), written to the other buffer
+//      at the new pitch, and the same values scattered into the dense B_w at
+//      (i, rlist[c]) -- so the dense B_w is k_fold's, entry for entry, and
+//      the operand is what k_bc_gather would gather from it;
+//   y_w += SY R over the group's columns, xw += U (R b) as k_fold.
+// The last workgroup resets the window and flips the active buffer.  The
+// grid is fixed (host-side, captured in graphs): workgroup b takes group
+// b % ng and row range b / ng of the floor(grid / ng) ranges; the rest only
+// count in.
+// ---------------------------------------------------------------------------
+template <int KW>
+__device__ __forceinline__ void cfold_tile_issue(const double* Bo, int64_t ldo, int S0, const double* U, int64_t c0,
+                                                 int64_t r0, int64_t i1, FoldTilePre<KW>& t) {
+    const int lane = threadIdx.x & 63;
+    const int kr = lane >> 4, cl = lane & 15;
+    const int64_t ilast = i1 > 0 ? i1 - 1 : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int64_t i0r = r0 + kr + 4 * r;
+        const int64_t i = i0r < ilast ? i0r : ilast;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t c = c0 + 32 * h + 2 * cl;  // even; the pair lies inside the old pitch when c < S0
+            t.b[r][h] = *reinterpret_cast<const fdbl2*>(&Bo[i * ldo + (c < S0 ? c : 0)]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KW / 8; ++j) {
+        const int e = 128 * j + 2 * lane;
+        const int64_t ia0 = r0 + e / KW;
+        const int64_t ia = ia0 < ilast ? ia0 : ilast;
+        t.u[j] = *reinterpret_cast<const fdbl2*>(&U[ia * KW + e % KW]);
+    }
+}
+// the old entries of the tile's columns, or e_k for the columns past S0
+// (rlv: rlist of this lane's four columns, -1 past S)
+__device__ __forceinline__ double cfold_old(double v, int64_t i, int64_t c, int S0, int k) {
+    return c < S0 ? v : (k == i ? 1.0 : 0.0);
+}
+
+template <int KW>
+__global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
+    static_assert(SPX_FOLD_ULDS, "the compact fold stages U through LDS");
+    DevState* st = P.st;
+    const int nw = st->nw;
+    if (nw < min_nw || nw < 2) return;
+    const int nf = nw - 1;
+    constexpr int KS = KW / 4;
+    __shared__ double Rl[KW][FOLD_RP];
+    __shared__ double NT[KW][FOLD_NP<KW>];
+    __shared__ double Ush[FOLD_THREADS / 64][16][FOLD_UP<KW>];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kr = lane >> 4, cl = lane & 15;
+    const int64_t L = P.L, m = P.m;
+    const int S = P.bc_n[0], sel = P.bc_n[2], S0 = P.bc_n[3];
+    const int64_t ldn = P.bc_n[1], ldo = P.bc_n[4] > 0 ? P.bc_n[4] : 64;
+    const double* const Bo = bc_buf(P, sel);
+    double* const Bn = bc_buf(P, sel ^ 1);
+    const int ng = (int)(ldn / 64);
+    const int nper = (int)gridDim.x / ng;  // row ranges per group
+    const int g = (int)blockIdx.x % ng, yr = (int)blockIdx.x / ng;
+    const bool work = yr < nper;
+    const int64_t c0 = (int64_t)g * 64;
+    const int64_t per = ((m + nper - 1) / nper + 15) / 16 * 16;
+    const int64_t i0 = work ? (int64_t)yr * per : m;
+    const int64_t i1 = (i0 + per < m) ? i0 + per : m;
+    if (work && i0 < m) {
+        // operands of R (this lane's column c0 + lane) and the coefficients
+        const int64_t cc = c0 + lane;
+        const int kc = cc < S ? P.rlist[cc] : 0;
+        double rq[KW];
+#pragma unroll
+        for (int t = 0; t < KW; ++t) rq[t] = (t < nf && cc < S && wave == 0) ? P.Qrows[(int64_t)t * L + kc] : 0.0;
+        FoldRPre<KW> rpre;
+#pragma unroll
+        for (int j = 0; j < FoldRPre<KW>::NPT; ++j) {
+            const int k = tid + j * FOLD_THREADS;
+            rpre.n[j] = P.Urows[k < KW * KW ? k : KW * KW - 1];
+        }
+        // the list entries of this lane's tile columns (unit entries past S0)
+        int rk[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const int64_t c = c0 + 32 * h + 2 * cl + x;
+                rk[2 * h + x] = c < S ? P.rlist[c] : -1;
+            }
+        // the wave's first tile in flight during the rebuild
+        const int64_t step = 16 * (int64_t)(FOLD_THREADS / 64);
+        int64_t r0 = i0 + 16 * wave;
+        FoldTilePre<KW> cur;
+        if (r0 < i1) cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
+        fold_stage_N_pre<KW>(rpre, nf, NT);
+        lds_barrier();
+        if (wave == 0) {
+            // right-looking, one lane per column: after step s, r_s is final and
+            // every r_t (t > s) has taken its s term (fold_rebuild_R4's fmas)
+#pragma unroll
+            for (int s = 0; s < KW - 1; ++s) {
+#pragma unroll
+                for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
+            }
+            const int sl = fold_slot(lane);
+#pragma unroll
+            for (int t = 0; t < KW; ++t) Rl[t][sl] = rq[t];
+        }
+        lds_barrier();
+        // tiles (fold_tiles' k-step order), the first one already in flight
+        double (*Us)[FOLD_UP<KW>] = Ush[wave];
+        for (; r0 < i1; r0 += step) {
+            dbl4 acc[4];
+            double af[KS];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = r0 + kr + 4 * r;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int64_t c = c0 + 32 * h + 2 * cl;
+                    cur.b[r][h].x = cfold_old(cur.b[r][h].x, i, c, S0, rk[2 * h]);
+                    cur.b[r][h].y = cfold_old(cur.b[r][h].y, i, c + 1, S0, rk[2 * h + 1]);
+                }
+            }
+            fold_tile_take<KW>(cur, r0, i1, nf, acc, af, Us);
+            if (r0 + step < i1) cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0 + step, i1, cur);
+            double rf[2][4];
+            double uf[2];
+            uf[0] = Us[cl][kr];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) rf[0][jb] = Rl[kr][16 * jb + cl];
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                if (s2 + 1 < KS) {
+                    uf[(s2 + 1) & 1] = Us[cl][4 * (s2 + 1) + kr];
+#pragma unroll
+                    for (int jb = 0; jb < 4; ++jb) rf[(s2 + 1) & 1][jb] = Rl[4 * (s2 + 1) + kr][16 * jb + cl];
+                }
+                const double a = uf[s2 & 1];
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, rf[s2 & 1][jb], acc[jb], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // the new operand rows (whole pitch: zeros past S) and the dense B_w
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = r0 + kr + 4 * r;
+                if (i < i1) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        fdbl2 v;
+                        v.x = acc[2 * h][r];
+                        v.y = acc[2 * h + 1][r];
+                        *reinterpret_cast<fdbl2*>(&Bn[i * ldn + c0 + 32 * h + 2 * cl]) = v;
+                        if (rk[2 * h] >= 0) P.B0[i * L + rk[2 * h]] = v.x;
+                        if (rk[2 * h + 1] >= 0) P.B0[i * L + rk[2 * h + 1]] = v.y;
+                    }
+                }
+            }
+        }
+        if (wave == 0 && yr == 0 && cc < S) {
+            // y_w += SY R for the group's columns (k_fold's sum, t ascending)
+            double* y = st->y_buf ? P.y1 : P.y0;
+            const int sl = fold_slot(lane);
+            double d = 0.0;
+#pragma unroll
+            for (int t = 0; t < KW; ++t)
+                if (t < nf) d = fma(P.SY[t], Rl[t][sl], d);
+            y[kc] += d;
+        }
+    }
+    if (wave == 1) {
+        // xw += U (R b), R b = Wt[n][0..nf): the rows spread over every
+        // workgroup, one lane per row, t ascending (k_fold's)
+        const double* wb = P.Wt + P.n * KW;
+        const int64_t nwg = (int64_t)gridDim.x;
+        const int64_t rpw = (m + nwg - 1) / nwg;
+        const int64_t r0 = (int64_t)blockIdx.x * rpw;
+        const int64_t r1 = (r0 + rpw < m) ? r0 + rpw : m;
+        for (int64_t i = r0 + lane; i < r1; i += 64) {
+            double d = 0.0;
+#pragma unroll
+            for (int t = 0; t < KW; ++t)
+                if (t < nf) d = fma(P.U[i * KW + t], wb[t], d);
+            P.xw[i] += d;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) s_last = arrive_last(arrive_group(P.arrive, ARR_FOLD), gridDim.x, blockIdx.x);
+    __syncthreads();
+    if (s_last && tid == 0) {
+        P.SY[0] = P.SY[nf];
+        P.bc_n[2] = sel ^ 1;
+        st->nw = 1;
+    }
+}
+
+// compact fold: k_bc_list (the window's leaving rows join the list) then
+// k_cfold over the listed columns only (P.bc, one workgroup per CU)
+hipError_t launch_cfold(const Params& P, int min_nw, int cus, hipStream_t s) {
+    hipLaunchKernelGGL(k_bc_list, dim3(1), dim3(1024), 0, s, P, min_nw);
+    // every column group of the list needs a workgroup (m > 16,384: more
+    // groups than CUs)
+    const int64_t ngmax = P.L / 64;
+    const int64_t nc = cus > 0 ? cus : 256;
+    const dim3 grid((unsigned)(nc > ngmax ? nc : ngmax));
+    switch (P.win) {
+        case 8: hipLaunchKernelGGL(k_cfold<8>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 16: hipLaunchKernelGGL(k_cfold<16>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 32: hipLaunchKernelGGL(k_cfold<32>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        case 64: hipLaunchKernelGGL(k_cfold<64>, grid, dim3(FOLD_THREADS), 0, s, P, min_nw); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -3280,7 +3537,7 @@ __global__ __launch_bounds__(256) void k_se_part(Params P) {
     __shared__ double sa[SE_RB];
     if (threadIdx.x < SE_RB) sa[threadIdx.x] = threadIdx.x < nr ? al[i0 + threadIdx.x] : 0.0;
     __syncthreads();
-    const double* Mw = P.bc ? P.bc : P.B0;
+    const double* Mw = P.bc ? bc_buf(P, P.bc_n[2]) : P.B0;
     const int64_t ldm = P.bc ? (int64_t)P.bc_n[1] : L;  // row pitch (compact: bc_pitch)
     double* out = P.se_part + (int64_t)blockIdx.x * (L + KW + 1);
     for (int c = threadIdx.x; c < ncols; c += blockDim.x) {

@@ -443,7 +443,7 @@ __global__ __launch_bounds__(BLOCK) void k_loop(Params P, LoopArgs La) {
             }
             auto compact_row = [&](int64_t i) -> double {
                 double a = (lane == 0 && P.rmap[i] < 0) ? apd[i] : 0.0;
-                const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc + i * (int64_t)P.bc_n[1]);
+                const dbl2* brow = reinterpret_cast<const dbl2*>(bc_buf(P, P.bc_n[2]) + i * (int64_t)P.bc_n[1]);
                 const int S2 = (Sb + 1) >> 1;
                 for (int k0 = 0; k0 < S2; k0 += 8 * 64) {
                     dbl2 v[8], w[8];

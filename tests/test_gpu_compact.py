@@ -213,3 +213,49 @@ def test_ftran_rows_per_wave_same_bits(spx, kw, rpw):
     for key in ("b_ixs", "x_b", "y", "binv"):
         assert np.array_equal(a[1][key], b[1][key]), key
     assert a[3].pivots == b[3].pivots and a[3].z == b[3].z
+
+
+@pytest.mark.parametrize("kw", [dict(m=401, n=1604, seed=11, window=64), dict(m=400, n=1600, seed=2, window=16),
+                                dict(m=1024, n=4096, seed=0, window=64), dict(m=300, n=1200, seed=8, window=32, pricing=1),
+                                dict(m=257, n=1001, seed=6, window=8, ratio_test=2),
+                                dict(m=300, n=1200, seed=3, window=64, pricing=2),
+                                dict(m=2051, n=6000, seed=5, window=64), dict(m=4096, n=16384, seed=0)],
+                         ids=["m401-w64", "m400-w16", "m1024-w64", "devex", "harris-w8", "steepest", "m2051", "C3"])
+def test_compact_fold_same_bits(spx, kw):
+    """The compact fold (k_cfold: the listed columns of B_w only, R rebuilt
+    one lane per column, the fold's MFMA tiles, the dense B_w kept by a
+    scatter) against the dense fold plus the gather (SPX_DENSE_FOLD=1): the
+    same R, the same tiles, so the same bits -- states, B^-1, traces and the
+    optimum -- through many folds, lists growing past several pitches of 64
+    and (at optimality) hundreds of columns."""
+    a = _run(spx, False, 300, persist=False, **kw)
+    with _env(SPX_DENSE_FOLD="1"):
+        b = _run(spx, False, 300, persist=False, **kw)
+    assert np.array_equal(a[2], b[2])
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    assert a[3].status == b[3].status and a[3].pivots == b[3].pivots and a[3].z == b[3].z
+
+
+def test_compact_fold_persistent_and_reinversion(spx, oracle):
+    """The compact fold between persistent k_loop launches, and a reinversion
+    (which regathers the operand into buffer 0 whichever buffer was active)
+    in the middle: the dense fold's bits, and the oracle's optimum."""
+    kw = dict(m=300, n=1200, seed=3, window=16)
+    outs = []
+    for dense in ("0", "1"):
+        with _env(SPX_DENSE_FOLD=dense):
+            with spx.Context(persist=True, trace=4096, **kw) as ctx:
+                ctx.iterate(37)
+                ctx.reinvert()
+                ctx.iterate(41)
+                s = ctx.state(binv=True)
+                r = ctx.solve()
+                outs.append((s, ctx.trace(), r))
+    (sa, ta, ra), (sb, tb, rb) = outs
+    assert np.array_equal(ta, tb)
+    for key in ("b_ixs", "x_b", "y", "binv"):
+        assert np.array_equal(sa[key], sb[key]), key
+    A, b, c = oracle.generate(kw["m"], kw["n"], kw["seed"])
+    o = oracle.solve(A, b, c, eps=1e-7)
+    assert ra.status == spx.SolveStatus.OptimumFound and abs(ra.z - o.z) <= 1e-9 * abs(o.z)

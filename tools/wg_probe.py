@@ -48,6 +48,8 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
         put("price_entry_to_tail_reduced", np.median(pa[:, 2] - pa[:, 0]))
         if os.environ.get("SPX_LIB", "").find("xfst") >= 0:  # (build with SPX_DIAG_FETCH_STAMP: clock 3 = partials in)
             put("price_entry_to_partials_in", np.median(pa[:, 3] - pa[:, 0]))
+        elif os.environ.get("SPX_LIB", "").find("xmrg") >= 0:  # (SPX_DIAG_MERGE_STAMP: clock 3 = wave reductions done)
+            put("price_entry_to_wave_reduced", np.median(pa[:, 3] - pa[:, 0]))
         else:
             put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
         put("price_span", pa[:, 1].max() - p0)
