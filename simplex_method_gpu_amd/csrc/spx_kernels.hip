@@ -50,6 +50,9 @@ namespace spx {
 #ifndef SPX_PRICE_CH
 #define SPX_PRICE_CH 8  // chunks of a column's start prefetched (8-wave workgroups)
 #endif
+#ifndef SPX_PRICE_DEEP
+#define SPX_PRICE_DEEP 0  // deferred tail: the first column's first 16 chunks requested before the reduction (A/B)
+#endif
 #ifndef SPX_PRICE_PIPE
 #define SPX_PRICE_PIPE 1  // eta-window pricing: two 8-chunk batches of a column in flight
 #endif
@@ -73,6 +76,9 @@ constexpr int BC_PF = SPX_BC_PF;
 constexpr int BC_PF2 = SPX_BC_PF2;  // chunks requested once S is known (up to 512 columns)
 constexpr int BC_APC = 8192;  // A_p gathered onto the list in LDS blocks of this many columns
 constexpr int BC_RL = 2;
+#ifndef SPX_FTRAN_TRIM
+#define SPX_FTRAN_TRIM 0  // k_ftran_bc: compact-row chunk 0 and U rows read only where used (A/B)
+#endif
 
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
 // launch, slot[1] += (last-workgroup ticket - start), slot[2] += tail duration.
@@ -197,6 +203,15 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     bool fresh = false;
     int32_t pk_a = -1, pk_b = -1;
     int64_t pv_a = 0, pv_b = 0;
+    constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
+    // SPX_PRICE_DEEP (deferred tail): the first column's first 2 CH chunks are
+    // requested as soon as the tail's record says which column this slot
+    // holds after the pivot's list edit -- before the partials are reduced
+    // and the base row staged -- so HBM streams during the prologue instead
+    // of idling (only the end-of-list slot depends on q; it is left out)
+    constexpr bool DEEP = SPX_PRICE_DEEP && WM != 3 && BLOCK <= 512 && CH == 8;
+    dbl2 vd0[DEEP ? CH : 1], vd1[DEEP ? CH : 1];
+    int64_t jdeep = -1;  // the column the deep prefetch holds (-1: none)
     // the bookkeeping's inputs for workgroup 0's thread 0, which applies them
     // after its columns (issued first, its stores would hold up the waits for
     // its own staging loads: vmcnt retires in order)
@@ -211,13 +226,28 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         // 256-thread workgroups hold two threads' partials of the FTRAN
         // tail's 512-thread shape (reduce_partial_pair: the same bits)
         constexpr bool PAIR = BLOCK == 256;
+        const TailRec R = *P.trec;  // (first: the deep prefetch waits for it alone)
         UpdPartial w0 = tid < P.tail_parts ? upd_fetch<true>(P, tid) : upd_empty();
         UpdPartial w1 = upd_empty();
         if constexpr (PAIR) {
             if (tid + BLOCK < P.tail_parts) w1 = upd_fetch<true>(P, tid + BLOCK);
         }
-        const TailRec R = *P.trec;
         fresh = R.fresh != 0;
+        if constexpr (DEEP) {
+            // slots below cnt0 hold the same column before and after the
+            // list edit, except p's slot R.kp, which takes the last entry
+            const int64_t L2d = P.L >> 1;
+            const int32_t cnt0 = fresh ? (R.kp >= 0 ? R.cnt - 1 : R.cnt) : S.nb_count;
+            if (idx0 < cnt0 && (L2d & 511) == 0 && L2d >= 2 * CH * 64) {
+                const int64_t jd = (fresh && R.kp >= 0 && idx0 == R.kp) ? (int64_t)R.last : j0;
+                const dbl2* cd = reinterpret_cast<const dbl2*>(P.A + jd * P.L);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) vd0[u] = ld2<SPX_NT_A>(&cd[lane + u * 64]);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) vd1[u] = ld2<SPX_NT_A>(&cd[CH * 64 + lane + u * 64]);
+                jdeep = jd;
+            }
+        }
         if (fresh) {
             __shared__ UpdPartial s_ured[PAIR ? 2 * WAVES : WAVES];
 #ifdef SPX_DIAG_FETCH_STAMP  // timing probe: when the partials have arrived (stored as the pw[3] clock)
@@ -359,8 +389,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // which stay in flight across the LDS fill and the barrier.  Every load
     // here is unconditional with a clamped index (rr is always a valid row),
     // so the fill waits for its own loads only, not for the A prefetch.
-    constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
     static_assert(CH >= 1 && CH <= 8, "the pipelined column loop consumes at most one 8-chunk batch of prefetch");
+    const bool deep_hit = DEEP && jdeep >= 0 && jdeep == j0;  // (else the first column goes the usual way)
     const bool pre = WM != 3 && idx0 < nb && L2 >= CH * 64;
     dbl2 yv[YB], rv[YB], vv[YB];
     double uqrow = 0.0;  // U[q][tid] for Urows (window, workgroup 0)
@@ -378,11 +408,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     __builtin_amdgcn_sched_barrier(0);  // (the scheduler would hoist the A loads)
     dbl2 v0[CH];
     if constexpr (WM != 3) {
-        const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
+        if (!deep_hit) {
+            const dbl2* c0 = reinterpret_cast<const dbl2*>(P.A + j0 * L);
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t k = lane + u * 64;
-            v0[u] = ld2<SPX_NT_A>(&c0[k < L2 ? k : L2 - 1]);
+            for (int u = 0; u < CH; ++u) {
+                const int64_t k = lane + u * 64;
+                v0[u] = ld2<SPX_NT_A>(&c0[k < L2 ? k : L2 - 1]);
+            }
         }
     }
     if (stage) {
@@ -591,9 +623,24 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             };
             int64_t kb = CH * 64;
             dbl2 vc[8];
+            if (DEEP && first && deep_hit) {
+                // the two deep-prefetched batches, the third requested first
+                kb = 2 * CH * 64;
+                if (kb < L2) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
-            consume(v0, CH, 0);
+                    for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+                }
+                consume(vd0, CH, 0);
+                consume(vd1, CH, CH * 64);
+                if (kb >= L2) {
+                    k = L2;
+                    return;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+                consume(v0, CH, 0);
+            }
             for (; kb + 8 * 64 < L2; kb += 8 * 64) {
                 dbl2 vn[8];
 #pragma unroll
@@ -2014,7 +2061,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
         cbv[r] = P.c_B[icl[r]];
         xb0[r] = P.x_b[icl[r]];
         bix[r] = P.b_ixs[icl[r]];
-        urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
+        if (!SPX_FTRAN_TRIM) urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
     }
     const double sxw_w = P.Wt[P.n * KW + (lane < KW ? lane : 0)];
     struct {
@@ -2045,13 +2092,18 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
 #pragma unroll
         for (int t = 0; t < NCH; ++t) {
             const int k2 = lane + 64 * t;
-            const int kk = (t == 0) ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
+            const int kk = (t == 0 && !SPX_FTRAN_TRIM) ? (k2 < L2 ? k2 : (int)L2 - 1)
+                                                       : ((2 * k2 < Sbc && k2 < L2) ? k2 : (t == 0 ? 0 : lane));
             pf[r][t] = brow[r][kk];
         }
     }
     const int64_t qp = Sv.q;
     const bool pend = Sv.nw > 0;
     const int tau = Sv.nw - 1;
+    if (SPX_FTRAN_TRIM) {  // U rows: the pivots of the window only (lanes < tau)
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) urow[r] = P.U[icl[r] * KW + (lane < tau ? lane : 0)];
+    }
     const double sxw_u = P.U[(pend ? qp : 0) * KW + (lane < KW ? lane : 0)];
     const double sx_x = P.xw[pend ? qp : 0];
     __builtin_amdgcn_sched_barrier(0);

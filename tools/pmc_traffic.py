@@ -12,7 +12,7 @@ import json
 import statistics
 
 
-KERNELS = ("k_price", "k_ftran_bc", "k_update", "k_tab_fold", "k_fold", "k_bc_gather")
+KERNELS = ("k_price", "k_ftran_bc", "k_update", "k_tab_fold", "k_cfold", "k_fold", "k_bc_gather")
 
 
 def per_kernel(path, counter):

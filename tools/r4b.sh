@@ -11,3 +11,9 @@ timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/benc
 grep '^{' $OUT/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['kernels']['k_fold'], d['solve_to_optimum']['iterations_per_s'], d['solve_to_optimum']['seconds'])"
 timeout -k 10 400 python3 -u bench.py --gpus 1 --config C5 --steps 63 --warmup 5 --no-explicit --no-tableau --no-cpu-baseline --no-steepest --no-sharded-pricing --no-solve-to-optimum > $OUT/bench_c5.log 2>&1 || { tail -30 $OUT/bench_c5.log; exit 1; }
 grep '^{' $OUT/bench_c5.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C5', d['value'], d['ms_per_step'], d['roofline']['frac'], d['kernels']['k_fold'])"
+timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_build/xtrim/libsimplex.so > $OUT/ab_trim.log 2>&1 || { tail -30 $OUT/ab_trim.log; exit 1; }
+cat $OUT/ab_trim.log
+timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_build/xdeep/libsimplex.so > $OUT/ab_deep.log 2>&1 || { tail -30 $OUT/ab_deep.log; exit 1; }
+cat $OUT/ab_deep.log
+SPX_LIB=simplex_method_gpu_amd/_build/xdeep/libsimplex.so timeout -k 10 600 python -u -m pytest tests/test_gpu_defer.py tests/test_gpu_configs.py tests/test_gpu_compact.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_deep.log 2>&1 || { tail -40 $OUT/pytest_deep.log; exit 1; }
+tail -2 $OUT/pytest_deep.log
