@@ -50,9 +50,66 @@ __device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
     else *p = v;
 }
 
+// Wave butterflies.  The partner of every step is lane ^ off, off = 32, 16,
+// .., 1 (the __shfl_xor order every consumer shares, so the bits of a sum do
+// not depend on the kernel computing it).  SPX_DPP_SUM = 1 moves the partner
+// values with permlane swaps (32, 16), DPP row rotation (8), two banked DPP
+// row shifts (4) and quad permutes (2, 1) instead of ds_bpermute: the same
+// pairs (tools/dpp_sum_check.hip), so the same bits, without the LDS-path
+// latency per step.
+#ifndef SPX_DPP_SUM
+#define SPX_DPP_SUM 0
+#endif
+#ifndef SPX_DPP_X4A
+#define SPX_DPP_X4A 0x104  // row_shl:4 (tools/dpp_sum_check.hip picks the direction)
+#define SPX_DPP_X4B 0x114  // row_shr:4
+#endif
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_mv(double old, double v) {
+    const long long o = __double_as_longlong(old), b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, RM, BM, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, RM, BM, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int OFF>
+__device__ __forceinline__ double xor_partner(double v) {
+    if constexpr (!SPX_DPP_SUM) {
+        return __shfl_xor(v, OFF, 64);
+    } else if constexpr (OFF == 32 || OFF == 16) {
+        const int lane = threadIdx.x & 63;
+        const long long b = __double_as_longlong(v);
+        const bool up = OFF == 32 ? lane >= 32 : ((lane >> 4) & 1) != 0;
+        int l, h;
+        if constexpr (OFF == 32) {
+            const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+            const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+            l = up ? lo[0] : lo[1];
+            h = up ? hi[0] : hi[1];
+        } else {
+            const auto lo = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+            l = up ? lo[0] : lo[1];
+            h = up ? hi[0] : hi[1];
+        }
+        return __longlong_as_double((long long)(((unsigned long long)(unsigned)h << 32) | (unsigned)l));
+    } else if constexpr (OFF == 8) {
+        return dpp_mv<0x128, 0xF, 0xF>(v, v);  // row_ror:8 (within 16 lanes: lane ^ 8)
+    } else if constexpr (OFF == 4) {
+        const double t = dpp_mv<SPX_DPP_X4A, 0xF, 0x5>(v, v);  // banks 0, 2 <- lane + 4
+        return dpp_mv<SPX_DPP_X4B, 0xF, 0xA>(t, v);            // banks 1, 3 <- lane - 4
+    } else if constexpr (OFF == 2) {
+        return dpp_mv<0x4E, 0xF, 0xF>(v, v);  // quad_perm [2,3,0,1]
+    } else {
+        return dpp_mv<0xB1, 0xF, 0xF>(v, v);  // quad_perm [1,0,3,2]
+    }
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    v += xor_partner<32>(v);
+    v += xor_partner<16>(v);
+    v += xor_partner<8>(v);
+    v += xor_partner<4>(v);
+    v += xor_partner<2>(v);
+    v += xor_partner<1>(v);
     return v;
 }
 // two butterflies interleaved (their cross-lane latencies overlap)
@@ -65,25 +122,37 @@ __device__ __forceinline__ double mul_nc(double a, double b) {
     return a * b;
 }
 
+template <int OFF>
+__device__ __forceinline__ void sum_step2(double& a, double& b) {
+    const double ta = xor_partner<OFF>(a);
+    const double tb = xor_partner<OFF>(b);
+    a += ta;
+    b += tb;
+}
+template <int OFF>
+__device__ __forceinline__ void sum_step3(double& a, double& b, double& c) {
+    const double ta = xor_partner<OFF>(a);
+    const double tb = xor_partner<OFF>(b);
+    const double tc = xor_partner<OFF>(c);
+    a += ta;
+    b += tb;
+    c += tc;
+}
 __device__ __forceinline__ void wave_sum3(double& a, double& b, double& c) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ta = __shfl_xor(a, off, 64);
-        const double tb = __shfl_xor(b, off, 64);
-        const double tc = __shfl_xor(c, off, 64);
-        a += ta;
-        b += tb;
-        c += tc;
-    }
+    sum_step3<32>(a, b, c);
+    sum_step3<16>(a, b, c);
+    sum_step3<8>(a, b, c);
+    sum_step3<4>(a, b, c);
+    sum_step3<2>(a, b, c);
+    sum_step3<1>(a, b, c);
 }
 __device__ __forceinline__ void wave_sum2(double& a, double& b) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const double ta = __shfl_xor(a, off, 64);
-        const double tb = __shfl_xor(b, off, 64);
-        a += ta;
-        b += tb;
-    }
+    sum_step2<32>(a, b);
+    sum_step2<16>(a, b);
+    sum_step2<8>(a, b);
+    sum_step2<4>(a, b);
+    sum_step2<2>(a, b);
+    sum_step2<1>(a, b);
 }
 
 // ---- DPP cross-lane moves (gfx9 encodings; VALU-rate, no LDS round trip).

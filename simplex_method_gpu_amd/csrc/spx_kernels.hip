@@ -2248,7 +2248,9 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
         }
         for (int c = cb + (cb == 0 ? BC_RL * BLOCK : 0) + tid; c < ce; c += BLOCK) apc[c - cb] = apd[P.rlist[c]];
         lds_barrier();
+#ifndef SPX_DIAG_FTRAN_SUM
         if (wgt && cb == 0) wgt[2] = rtime();
+#endif
         const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -2301,14 +2303,26 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
 
     // ---- x_b += s_x E (v4:348), alpha_i, theta_i (v4:199-208), the partials
     // (the RPW rows' butterflies interleaved: each value's own bits)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
+    auto rows_step = [&](auto off_t) {
+        constexpr int OFF = decltype(off_t)::value;
         double t[RPW];
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) t[r] = __shfl_xor(acc[r], off, 64);
+        for (int r = 0; r < RPW; ++r) t[r] = xor_partner<OFF>(acc[r]);
 #pragma unroll
         for (int r = 0; r < RPW; ++r) acc[r] += t[r];
+    };
+    rows_step(std::integral_constant<int, 32>());
+    rows_step(std::integral_constant<int, 16>());
+    rows_step(std::integral_constant<int, 8>());
+    rows_step(std::integral_constant<int, 4>());
+    rows_step(std::integral_constant<int, 2>());
+    rows_step(std::integral_constant<int, 1>());
+#ifdef SPX_DIAG_FTRAN_SUM  // timing probe: clock 2 = the row sums are done (in place of A_p in LDS)
+    if (wgt) {
+        asm volatile("" ::"v"(acc[0]), "v"(sxw));
+        wgt[2] = rtime();
     }
+#endif
     UpdPartial wp[RPW];
     double al[RPW], xb[RPW];
 #pragma unroll

@@ -17,3 +17,11 @@ timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_bu
 cat $OUT/ab_deep.log
 SPX_LIB=simplex_method_gpu_amd/_build/xdeep/libsimplex.so timeout -k 10 600 python -u -m pytest tests/test_gpu_defer.py tests/test_gpu_configs.py tests/test_gpu_compact.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_deep.log 2>&1 || { tail -40 $OUT/pytest_deep.log; exit 1; }
 tail -2 $OUT/pytest_deep.log
+SPX_LIB=simplex_method_gpu_amd/_build/xfsum/libsimplex.so timeout -k 10 120 python3 -u tools/wg_probe.py > $OUT/wg_probe_fsum.json 2>&1 || { tail -30 $OUT/wg_probe_fsum.json; exit 1; }
+head -60 $OUT/wg_probe_fsum.json | grep -A3 ftran
+timeout -k 10 400 python3 -u tools/ab.py --m 16384 --n 65536 --k 126 --warm 64 --rounds 3 --variants '[{}, {"_env": {"SPX_DENSE_FOLD": "1"}}, {"_env": {"SPX_FTRAN_RPW": "2"}}, {"_env": {"SPX_FTRAN_RPW": "4"}}]' > $OUT/ab_c5.log 2>&1 || { tail -30 $OUT/ab_c5.log; exit 1; }
+tail -8 $OUT/ab_c5.log
+timeout -k 10 60 ./tools/dpp_sum_check > $OUT/dpp_sum_check.log 2>&1 || { cat $OUT/dpp_sum_check.log; exit 1; }
+cat $OUT/dpp_sum_check.log
+timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_build/xdpp/libsimplex.so > $OUT/ab_dpp.log 2>&1 || { tail -30 $OUT/ab_dpp.log; exit 1; }
+cat $OUT/ab_dpp.log

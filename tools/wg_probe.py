@@ -58,8 +58,12 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
         put("price_end_to_ftran_entry", f0 - pa[:, 1].max())
         put("ftran_entry_spread", fa[:, 0].max() - f0)
         put("ftran_entry_to_p", np.median(fa[:, 1] - fa[:, 0]))
-        put("ftran_p_to_ap_lds", np.median(fa[:, 2] - fa[:, 1]))
-        put("ftran_ap_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
+        if os.environ.get("SPX_LIB", "").find("xfsum") >= 0:  # (SPX_DIAG_FTRAN_SUM: clock 2 = row sums done)
+            put("ftran_p_to_sums_done", np.median(fa[:, 2] - fa[:, 1]))
+            put("ftran_sums_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
+        else:
+            put("ftran_p_to_ap_lds", np.median(fa[:, 2] - fa[:, 1]))
+            put("ftran_ap_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
         put("ftran_publish_max", fa[:, 3].max() - f0)
         if A["tail"] > fa[:, 3].max():  # the FTRAN pass ran the tail itself
             put("publish_max_to_tail", int(A["tail"]) - fa[:, 3].max())
