@@ -277,9 +277,15 @@ def main():
     price_bytes_all = reduce_sum([ks["price_bytes"]])[0]
     price_gbs = ks["price_bytes"] / (ks["price_ms"] * 1e-3) / 1e9 if ks["price_ms"] > 0 else 0.0
     update_gbs = ks["update_bytes"] / (ks["update_ms"] * 1e-3) / 1e9 if ks["update_ms"] > 0 else 0.0
-    # fold: B_w read + written, U / Qrows read once per window
-    fold_bytes = 16.0 * m * m + 8.0 * win * 2 * m if win else 0.0
-    b_upd = 8.0 * m * ev_run["ftran_cols"] + 16.0 * m * m / (win - 1) if win else 16.0 * m * m
+    # fold: dense -- B_w read + written, U / Qrows read once
+    # per window; compact (k_cfold) -- the operand's S columns read, written
+    # and scattered into the dense B_w, U read once
+    S_end = ev_run["ftran_cols"]
+    if win and cfg.get("compact_fold"):
+        fold_bytes = 8.0 * m * (3.0 * S_end + win)
+    else:
+        fold_bytes = 16.0 * m * m + 8.0 * win * 2 * m if win else 0.0
+    b_upd = 8.0 * m * S_end + fold_bytes / (win - 1) if win else 16.0 * m * m
     b_moved = price_bytes_all + b_upd                       # this representation, per pivot
     b_alg = 8.0 * (m + 1) * (n - m) + 16.0 * m * m         # SURVEY.md §8(d) B_alg, per pivot
 
@@ -395,7 +401,9 @@ def main():
                                       else "FTRAN (B_w read-only) + ratio test"),
                              "avg_launch_ms": ks["update_ms"], "algorithmic_bytes_per_launch": ks["update_bytes"],
                              "achieved_GBps": update_gbs, "frac": update_gbs / HBM_PEAK_GBS},
-                "k_fold": ({"avg_launch_ms": ks["fold_ms"], "launches_timed": ks["folds"],
+                "k_fold": ({"kernels": ("k_bc_list + k_cfold (the listed columns of B_w only)"
+                                        if cfg.get("compact_fold") else "k_fold + k_bc_list + k_bc_gather"),
+                            "avg_launch_ms": ks["fold_ms"], "launches_timed": ks["folds"],
                             "per_pivot_ms": ks["fold_ms"] / (win - 1),
                             "algorithmic_bytes_per_launch": fold_bytes,
                             "achieved_GBps": fold_bytes / (ks["fold_ms"] * 1e-3) / 1e9 if ks["fold_ms"] > 0 else 0.0}

@@ -390,8 +390,10 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * (SPX_FLAG_TABLEAU) in use, [11] workgroups of the persistent loop kernel,
  * [12] the ratio-test tail deferred into the next pricing pass (1; compact
  * window passes on one rank, SPX_DEFER_TAIL=0 turns it off) or run by the
- * FTRAN pass's last workgroup (0). */
-#define SPX_CONFIG_FIELDS 13
+ * FTRAN pass's last workgroup (0), [13] the window fold updates only B_w's
+ * listed (non-unit) columns (1: k_cfold; SPX_DENSE_FOLD=1 turns it off) or
+ * the dense B_w (0), [14] k_ftran_bc rows per wave (0: not in use). */
+#define SPX_CONFIG_FIELDS 15
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Columns of B^-1 the FTRAN stream reads per row: m, or with the eta window's

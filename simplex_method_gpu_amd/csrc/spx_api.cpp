@@ -1763,7 +1763,10 @@ int spx_info(spx_ctx* x, int64_t* m, int64_t* n, int64_t* ld, int64_t* local_nb,
     int32_t cols = 0;
     SPX_TRY(spx_ftran_cols(x, &cols));
     const double md = (double)x->m;
-    if (bu) *bu = x->P.win ? 8.0 * md * (double)cols + 16.0 * md * md / (x->P.win - 1) : 16.0 * md * md;
+    // the fold per window: dense -- B_w read + written; compact (k_cfold) --
+    // the operand's columns read, written and scattered into B_w, U read
+    const double fold = (x->P.bc && x->P.cfold) ? 8.0 * md * (3.0 * cols + x->P.win) : 16.0 * md * md;
+    if (bu) *bu = x->P.win ? 8.0 * md * (double)cols + fold / (x->P.win - 1) : 16.0 * md * md;
     return SPX_OK;
 }
 
@@ -1792,6 +1795,8 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[10] = x->P.tab;
     out[11] = x->persist ? x->lcfg.grid : 0;
     out[12] = x->defer_tail ? 1 : 0;
+    out[13] = (x->P.bc && x->P.cfold) ? 1 : 0;
+    out[14] = (x->P.bc && x->ucfg.rows == 1 && x->ucfg.bc_entry) ? x->ucfg.bc_entry : 0;
     return SPX_OK;
 }
 

@@ -58,7 +58,7 @@ __device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
 // pairs (tools/dpp_sum_check.hip), so the same bits, without the LDS-path
 // latency per step.
 #ifndef SPX_DPP_SUM
-#define SPX_DPP_SUM 0
+#define SPX_DPP_SUM 1
 #endif
 #ifndef SPX_DPP_X4A
 #define SPX_DPP_X4A 0x104  // row_shl:4 (tools/dpp_sum_check.hip picks the direction)

@@ -50,8 +50,14 @@ namespace spx {
 #ifndef SPX_PRICE_CH
 #define SPX_PRICE_CH 8  // chunks of a column's start prefetched (8-wave workgroups)
 #endif
+#ifndef SPX_CFOLD_RB
+#define SPX_CFOLD_RB 0  // k_cfold: R rebuilt in row blocks of this size (0: right-looking)
+#endif
+#ifndef SPX_MERGE1
+#define SPX_MERGE1 0  // deferred tail: one wave merges the wave partials and hands the result on (A/B)
+#endif
 #ifndef SPX_PRICE_DEEP
-#define SPX_PRICE_DEEP 0  // deferred tail: the first column's first 16 chunks requested before the reduction (A/B)
+#define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
 #ifndef SPX_PRICE_PIPE
 #define SPX_PRICE_PIPE 1  // eta-window pricing: two 8-chunk batches of a column in flight
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             }
         }
         if (fresh) {
-            __shared__ UpdPartial s_ured[PAIR ? 2 * WAVES : WAVES];
+            __shared__ UpdPartial s_ured[(PAIR ? 2 * WAVES : WAVES) + 1];
 #ifdef SPX_DIAG_FETCH_STAMP  // timing probe: when the partials have arrived (stored as the pw[3] clock)
             {
                 const int g0 = tid < P.tail_parts ? tid : 0;
@@ -1113,7 +1119,22 @@ __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, 
     const UpdPartial o = wave_reduce_partial(w);
     if (lane == 0) red[wave] = o;
     lds_barrier();
-    if constexpr (PLAIN) {
+    if constexpr (PLAIN && SPX_MERGE1) {
+        // wave 0 merges (the same order) and hands the result to the other
+        // waves through one more LDS slot: one wave reads the WAVES partials
+        // instead of every wave (the callers' arrays hold WAVES + 1)
+        if (wave == 0) {
+            UpdPartial r[WAVES];
+#pragma unroll
+            for (int k = 0; k < WAVES; ++k) r[k] = red[k];
+            UpdPartial t = r[0];
+#pragma unroll
+            for (int k = 1; k < WAVES; ++k) upd_merge_sel(t, r[k]);
+            if (lane == 0) red[WAVES] = t;
+        }
+        lds_barrier();
+        return red[WAVES];
+    } else if constexpr (PLAIN) {
         // the deferred tail (k_price's prologue, k_apply_tail): every wave
         // partial requested before a branch-free merge, and no closing
         // barrier (the callers pass an LDS array of their own).  (In the
@@ -1342,7 +1363,7 @@ __global__ __launch_bounds__(512) void k_apply_tail(Params P) {
     const TailRec R = *P.trec;
     if (!R.fresh) return;
     if (R.it == st->iter) {  // not yet applied by a pricing pass
-        __shared__ UpdPartial s_ured[8];
+        __shared__ UpdPartial s_ured[9];
         const UpdPartial t = reduce_update_partials<512, true>(P, s_ured, P.tail_parts);
         if (threadIdx.x == 0) apply_deferred_tail(P, st, R, t);
     }
@@ -3327,12 +3348,34 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         fold_stage_N_pre<KW>(rpre, nf, NT);
         lds_barrier();
         if (wave == 0) {
-            // right-looking, one lane per column: after step s, r_s is final and
-            // every r_t (t > s) has taken its s term (fold_rebuild_R4's fmas)
+            // one lane per column; every r_t takes its s terms in ascending s
+            // (fold_rebuild_R4's fmas, so its bits)
+            if constexpr (SPX_CFOLD_RB > 0) {
+                // rows in blocks of RB: the finished rows' terms as RB
+                // independent chains per step (their coefficients one
+                // contiguous LDS read), then the block's own triangle
+                constexpr int RB = SPX_CFOLD_RB;
 #pragma unroll
-            for (int s = 0; s < KW - 1; ++s) {
+                for (int t0 = 0; t0 < KW; t0 += RB) {
 #pragma unroll
-                for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
+                    for (int s = 0; s < t0; ++s) {
+#pragma unroll
+                        for (int j = 0; j < RB; ++j) rq[t0 + j] = fma(NT[s][t0 + j], rq[s], rq[t0 + j]);
+                    }
+#pragma unroll
+                    for (int s = t0; s < t0 + RB - 1; ++s) {
+#pragma unroll
+                        for (int t = s + 1; t < t0 + RB; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
+                    }
+                }
+            } else {
+                // right-looking: after step s, r_s is final and every r_t
+                // (t > s) has taken its s term
+#pragma unroll
+                for (int s = 0; s < KW - 1; ++s) {
+#pragma unroll
+                    for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
+                }
             }
             const int sl = fold_slot(lane);
 #pragma unroll

@@ -1,0 +1,21 @@
+# round-4 evidence: every -m gpu test, smoke(), the bench with the driver's
+# arguments (3 runs), the other configs, the rocprofv3 kernel trace of the
+# bench and the PMC traffic passes (tools/gpu_profile.sh)
+set -o pipefail
+OUT=gpurun_out/r4final
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+tail -3 $OUT/pytest.log
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+tail -2 $OUT/smoke.log
+for i in 1 2 3; do
+timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_$i.log 2>&1 || { tail -30 $OUT/bench_$i.log; exit 1; }
+grep '^{' $OUT/bench_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C3', d['value'], d['ms_per_step'], d['roofline']['frac'], d['solve_to_optimum']['iterations_per_s'], d['steepest']['solve']['pivots'])"
+done
+for C in C2 C4 C5; do
+X=""; [ $C != C2 ] && X="--no-solve-to-optimum --no-steepest"
+timeout -k 10 500 python3 -u bench.py --gpus 1 --config $C --steps 126 --warmup 5 --no-cpu-baseline --no-sharded-pricing $X > $OUT/bench_$C.log 2>&1 || { tail -30 $OUT/bench_$C.log; exit 1; }
+grep '^{' $OUT/bench_$C.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$C', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+done
+timeout -k 10 1000 bash tools/gpu_profile.sh r04 > $OUT/profile.log 2>&1 || { tail -30 $OUT/profile.log; exit 1; }
+tail -15 $OUT/profile.log

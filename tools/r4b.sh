@@ -25,3 +25,5 @@ timeout -k 10 60 ./tools/dpp_sum_check > $OUT/dpp_sum_check.log 2>&1 || { cat $O
 cat $OUT/dpp_sum_check.log
 timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_build/xdpp/libsimplex.so > $OUT/ab_dpp.log 2>&1 || { tail -30 $OUT/ab_dpp.log; exit 1; }
 cat $OUT/ab_dpp.log
+timeout -k 10 300 python3 -u tools/pass_ab.py default simplex_method_gpu_amd/_build/xmerge1/libsimplex.so > $OUT/ab_merge1.log 2>&1 || { tail -30 $OUT/ab_merge1.log; exit 1; }
+cat $OUT/ab_merge1.log
