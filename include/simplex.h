@@ -349,6 +349,12 @@ int spx_pass_times(spx_ctx* ctx, double out[3], int64_t* passes);
 #define SPX_PHASES 18
 int spx_phase_times(spx_ctx* ctx, double out[SPX_PHASES]);
 
+/* With SPX_FLAG_STAMPS: the compact fold's (k_cfold) per-workgroup clocks of
+ * its last launch, 8 words per workgroup (up to 1024 workgroups): entry,
+ * coefficients staged, R in LDS, tiles done, the y / xw updates done, the
+ * arrival counted (s_memrealtime, 100 MHz).  count = words written. */
+int spx_fold_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
+
 /* Diagnostic (SPX_FLAG_STAMPS, compact window passes): the clocks of the
  * last two passes, s_memrealtime ticks (100 MHz), one block per pass parity
  * (iteration & 1, parity 0 first).  A block holds, per workgroup g of that

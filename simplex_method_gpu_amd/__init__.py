@@ -349,6 +349,16 @@ class Context:
                         "tail": int(b[nu + npr]), "mark": int(b[nu + npr + 1])})
         return res
 
+    def fold_times(self):
+        """The compact fold's per-workgroup clocks of its last launch (stamps=True,
+        spx_fold_times): (workgroups, 6) ticks -- entry, coefficients staged,
+        R in LDS, tiles done, vectors done, arrival counted; zero rows for
+        workgroups past the grid."""
+        out = np.zeros(8 * 1024, dtype=np.uint64)
+        cnt = ctypes.c_int64()
+        check(self._L.spx_fold_times(self._h, _ptr(out), out.size, ctypes.byref(cnt)))
+        return out.reshape(1024, 8)[:, :6]
+
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""
         out = (ctypes.c_double * 18)()

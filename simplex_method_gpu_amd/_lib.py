@@ -74,6 +74,7 @@ SIGNATURES = {
     "spx_config": (ctypes.c_int, [_p, _p]),
     "spx_phase_times": (ctypes.c_int, [_p, _p]),
     "spx_wg_times": (ctypes.c_int, [_p, _p, _i64, _p]),
+    "spx_fold_times": (ctypes.c_int, [_p, _p, _i64, _p]),
     "spx_loop_times": (ctypes.c_int, [_p, _p, _p]),
     "spx_shard_range": (ctypes.c_int, [_i64, _i64, _i32, _i32, _p]),
     "spx_minloc_merge": (ctypes.c_int, [_p, _p, _i32, _p, _p]),

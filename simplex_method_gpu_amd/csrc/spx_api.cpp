@@ -1505,6 +1505,16 @@ int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
     return SPX_OK;
 }
 
+int spx_fold_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
+    if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
+    if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
+    HIP_TRY(hipStreamSynchronize(x->stream));
+    const int64_t n = std::min<int64_t>(cap, (int64_t)STAMP_FOLD_PER * 1024);
+    HIP_TRY(hipMemcpy(out, x->P.stamps + STAMP_FOLD, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost));
+    if (count) *count = n;
+    return SPX_OK;
+}
+
 int spx_get_weights(spx_ctx* x, double* w) {
     if (!x || !w) return fail(SPX_ERR_ARG, "NULL argument");
     if (!x->P.W) return fail(SPX_ERR_STATE, "no pricing weights: the context runs Dantzig pricing");

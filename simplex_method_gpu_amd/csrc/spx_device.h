@@ -173,7 +173,11 @@ __host__ __device__ inline bool argmin_better(double v, int64_t j, double bv, in
 constexpr int64_t STAMP_FTRAN = 32;
 constexpr int64_t STAMP_PRICE = STAMP_FTRAN + 2 * 4 * 4096;
 constexpr int64_t STAMP_TAIL = STAMP_PRICE + 2 * 4 * 4096;
-constexpr int64_t STAMP_WORDS = STAMP_TAIL + 8;
+// the compact fold's per-workgroup clocks (k_cfold, up to 1024 workgroups):
+// entry, coefficients staged, R in LDS, tiles done, vectors done, arrived
+constexpr int64_t STAMP_FOLD = STAMP_TAIL + 8;
+constexpr int STAMP_FOLD_PER = 8;
+constexpr int64_t STAMP_WORDS = STAMP_FOLD + STAMP_FOLD_PER * 1024;
 
 struct Params {
     // problem

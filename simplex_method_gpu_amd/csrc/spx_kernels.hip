@@ -3314,6 +3314,10 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
     const int nper = (int)gridDim.x / ng;  // row ranges per group
     const int g = (int)blockIdx.x % ng, yr = (int)blockIdx.x / ng;
     const bool work = yr < nper;
+    unsigned long long* const fst =
+        (P.stamps && tid == 0 && blockIdx.x < 1024) ? P.stamps + STAMP_FOLD + STAMP_FOLD_PER * (int64_t)blockIdx.x
+                                                    : nullptr;
+    if (fst) fst[0] = rtime();
     const int64_t c0 = (int64_t)g * 64;
     const int64_t per = ((m + nper - 1) / nper + 15) / 16 * 16;
     const int64_t i0 = work ? (int64_t)yr * per : m;
@@ -3347,6 +3351,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         if (r0 < i1) cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
         fold_stage_N_pre<KW>(rpre, nf, NT);
         lds_barrier();
+        if (fst) fst[1] = rtime();
         if (wave == 0) {
             // one lane per column; every r_t takes its s terms in ascending s
             // (fold_rebuild_R4's fmas, so its bits)
@@ -3382,6 +3387,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
             for (int t = 0; t < KW; ++t) Rl[t][sl] = rq[t];
         }
         lds_barrier();
+        if (fst) fst[2] = rtime();
         // tiles (fold_tiles' k-step order), the first one already in flight
         double (*Us)[FOLD_UP<KW>] = Ush[wave];
         for (; r0 < i1; r0 += step) {
@@ -3434,6 +3440,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
                 }
             }
         }
+        if (fst) fst[3] = rtime();
         if (wave == 0 && yr == 0 && cc < S) {
             // y_w += SY R for the group's columns (k_fold's sum, t ascending)
             double* y = st->y_buf ? P.y1 : P.y0;
@@ -3462,8 +3469,10 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         }
     }
     __syncthreads();
+    if (fst) fst[4] = rtime();
     if (tid == 0) s_last = arrive_last(arrive_group(P.arrive, ARR_FOLD), gridDim.x, blockIdx.x);
     __syncthreads();
+    if (fst) fst[5] = rtime();
     if (s_last && tid == 0) {
         P.SY[0] = P.SY[nf];
         P.bc_n[2] = sel ^ 1;
