@@ -192,12 +192,11 @@ def main():
         if kw:
             ds = ctx.dispatch_stats()
             lead = (kw - ds["window_pos"]) if ds["window_pos"] < kw else 0
-            ctx.iterate(lead)  # the next pass starts with a fold
+        info0 = ctx.info()  # (readbacks first: the lead passes run right before the timed region)
+        _, piv0 = ctx.iterate(lead)  # the next pass starts with a fold
         if events:
-            ctx.pass_times()  # drop the warm-up's events
+            ctx.pass_times()  # drop the warm-up's and the lead's events
             ctx.loop_times()
-        info0 = ctx.info()
-        _, piv0 = ctx.iterate(0)
         d0 = ctx.dispatch_stats()
         barrier()
         torch.cuda.synchronize()

@@ -351,13 +351,14 @@ class Context:
 
     def fold_times(self):
         """The compact fold's per-workgroup clocks of its last launch (stamps=True,
-        spx_fold_times): (workgroups, 6) ticks -- entry, coefficients staged,
-        R in LDS, tiles done, vectors done, arrival counted; zero rows for
-        workgroups past the grid."""
+        spx_fold_times): (workgroups, 8) ticks -- entry, coefficients staged,
+        R in LDS, tiles done, vectors done, arrival counted, (unused), then
+        the xw wave's end and the y wave's end (row-range-0 workgroups); zero
+        for workgroups past the grid."""
         out = np.zeros(8 * 1024, dtype=np.uint64)
         cnt = ctypes.c_int64()
         check(self._L.spx_fold_times(self._h, _ptr(out), out.size, ctypes.byref(cnt)))
-        return out.reshape(1024, 8)[:, :6]
+        return out.reshape(1024, 8)
 
     def phase_times(self):
         """In-kernel phase split (needs stamps=True), microseconds summed."""

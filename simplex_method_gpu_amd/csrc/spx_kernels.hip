@@ -50,8 +50,11 @@ namespace spx {
 #ifndef SPX_PRICE_CH
 #define SPX_PRICE_CH 8  // chunks of a column's start prefetched (8-wave workgroups)
 #endif
-#ifndef SPX_CFOLD_RB
-#define SPX_CFOLD_RB 0  // k_cfold: R rebuilt in row blocks of this size (0: right-looking)
+#ifndef SPX_CFOLD_T
+#define SPX_CFOLD_T 1  // k_cfold: R rebuilt one lane per row, 8 columns per wave (0: one lane per column)
+#endif
+#ifndef SPX_CFOLD_EXEC
+#define SPX_CFOLD_EXEC 1  // k_cfold (SPX_CFOLD_T): lanes t <= s masked per step by exec (0: a select per fma)
 #endif
 #ifndef SPX_MERGE1
 #define SPX_MERGE1 0  // deferred tail: one wave merges the wave partials and hands the result on (A/B)
@@ -3294,7 +3297,11 @@ template <int KW>
 __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
     static_assert(SPX_FOLD_ULDS, "the compact fold stages U through LDS");
     DevState* st = P.st;
+    // (the list's shape read beside the window count: one round trip)
     const int nw = st->nw;
+    const int S = P.bc_n[0], sel = P.bc_n[2], S0 = P.bc_n[3];
+    const int64_t ldn = P.bc_n[1], ldo = P.bc_n[4] > 0 ? P.bc_n[4] : 64;
+    asm volatile("" ::"s"(S), "s"(sel), "s"(S0), "s"(ldn), "s"(ldo));  // (kept ahead of the branch)
     if (nw < min_nw || nw < 2) return;
     const int nf = nw - 1;
     constexpr int KS = KW / 4;
@@ -3306,8 +3313,6 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kr = lane >> 4, cl = lane & 15;
     const int64_t L = P.L, m = P.m;
-    const int S = P.bc_n[0], sel = P.bc_n[2], S0 = P.bc_n[3];
-    const int64_t ldn = P.bc_n[1], ldo = P.bc_n[4] > 0 ? P.bc_n[4] : 64;
     const double* const Bo = bc_buf(P, sel);
     double* const Bn = bc_buf(P, sel ^ 1);
     const int ng = (int)(ldn / 64);
@@ -3317,15 +3322,54 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
     unsigned long long* const fst =
         (P.stamps && tid == 0 && blockIdx.x < 1024) ? P.stamps + STAMP_FOLD + STAMP_FOLD_PER * (int64_t)blockIdx.x
                                                     : nullptr;
+    // (lane 0 of every wave: the y / xw waves' own end stamps, slots 7 / 6)
+    unsigned long long* const fsx =
+        (P.stamps && lane == 0 && blockIdx.x < 1024) ? P.stamps + STAMP_FOLD + STAMP_FOLD_PER * (int64_t)blockIdx.x
+                                                     : nullptr;
     if (fst) fst[0] = rtime();
     const int64_t c0 = (int64_t)g * 64;
     const int64_t per = ((m + nper - 1) / nper + 15) / 16 * 16;
     const int64_t i0 = work ? (int64_t)yr * per : m;
     const int64_t i1 = (i0 + per < m) ? i0 + per : m;
     if (work && i0 < m) {
-        // operands of R (this lane's column c0 + lane) and the coefficients
         const int64_t cc = c0 + lane;
-        const int kc = cc < S ? P.rlist[cc] : 0;
+        // (the list entry of this lane's column, for y_w: read unconditionally
+        // and pinned below, so the compiler cannot turn it into a guarded
+        // load waited for on the spot)
+        int kcl = P.rlist[cc < L ? cc : L - 1];
+#if SPX_CFOLD_T
+        // R, one lane per row t and eight columns per wave (columns
+        // c0 + 8 wave + j): lane t holds N[t][s] = Urows[t][s] (0 unless
+        // s < t < nf) and r_t of each column; step s hands r_s (final after
+        // step s - 1) from lane s to the lanes t > s, which take
+        // fma(N[t][s], r_s, r_t) -- every r_t its s terms in ascending s,
+        // fold_rebuild_R4's fma sequence, so its bits
+        constexpr int CPW = 64 / (FOLD_THREADS / 64);
+        const int64_t cw0 = c0 + CPW * wave;
+        const bool rows = cw0 < S;  // (wave-uniform) any listed column
+        const int tl = lane < KW ? lane : KW - 1;
+        double rt[CPW];
+        // every operand read unconditionally (clamped): the coefficients
+        // (staged transposed into LDS, NT[s][t] = N[t][s], as k_fold), the
+        // list entries, then the base-row entries, which wait only for the
+        // first two (vmcnt retires in issue order)
+        FoldRPre<KW> rpre;
+#pragma unroll
+        for (int j = 0; j < FoldRPre<KW>::NPT; ++j) {
+            const int k = tid + j * FOLD_THREADS;
+            rpre.n[j] = P.Urows[k < KW * KW ? k : KW * KW - 1];
+        }
+        int kl[CPW];
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) kl[j] = P.rlist[cw0 + j < L ? cw0 + j : L - 1];
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) {
+            const int k = (unsigned)kl[j] < (unsigned)L ? kl[j] : 0;
+            rt[j] = P.Qrows[(int64_t)tl * L + k];
+        }
+#else
+        // operands of R (this lane's column c0 + lane) and the coefficients
+        const int kc = cc < S ? kcl : 0;
         double rq[KW];
 #pragma unroll
         for (int t = 0; t < KW; ++t) rq[t] = (t < nf && cc < S && wave == 0) ? P.Qrows[(int64_t)t * L + kc] : 0.0;
@@ -3335,6 +3379,7 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
             const int k = tid + j * FOLD_THREADS;
             rpre.n[j] = P.Urows[k < KW * KW ? k : KW * KW - 1];
         }
+#endif
         // the list entries of this lane's tile columns (unit entries past S0)
         int rk[4];
 #pragma unroll
@@ -3348,44 +3393,69 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         const int64_t step = 16 * (int64_t)(FOLD_THREADS / 64);
         int64_t r0 = i0 + 16 * wave;
         FoldTilePre<KW> cur;
+#if SPX_CFOLD_T
+        // (unconditional: rows clamped into the range, a branch here made
+        // the compiler wait for everything before the rebuild)
+        cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
+        fold_stage_N_pre<KW>(rpre, nf, NT);
+        lds_barrier();
+        // (the pins: every read above is issued before anything waits)
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) {
+            asm volatile("" : "+v"(rt[j]));
+            rt[j] = (lane < nf && cw0 + j < S) ? rt[j] : 0.0;
+        }
+        asm volatile("" : "+v"(kcl));
+        if (fst) fst[1] = rtime();
+        if (rows) {
+#pragma unroll
+            for (int s = 0; s < KW - 1; ++s) {
+                const double co = NT[s][tl];
+                if constexpr (SPX_CFOLD_EXEC) {
+                    // one exec mask per step for the wave's columns
+                    double rs[CPW];
+#pragma unroll
+                    for (int j = 0; j < CPW; ++j) rs[j] = readlane_d(rt[j], s);
+                    if (lane > s) {
+#pragma unroll
+                        for (int j = 0; j < CPW; ++j) rt[j] = fma(co, rs[j], rt[j]);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < CPW; ++j) {
+                        const double rs = readlane_d(rt[j], s);
+                        const double v = fma(co, rs, rt[j]);
+                        rt[j] = lane > s ? v : rt[j];
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < CPW; ++j) rt[j] = 0.0;
+        }
+        if (lane < KW) {
+#pragma unroll
+            for (int j = 0; j < CPW; ++j) Rl[lane][fold_slot(CPW * wave + j)] = rt[j];
+        }
+#else
         if (r0 < i1) cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
         fold_stage_N_pre<KW>(rpre, nf, NT);
         lds_barrier();
         if (fst) fst[1] = rtime();
         if (wave == 0) {
-            // one lane per column; every r_t takes its s terms in ascending s
-            // (fold_rebuild_R4's fmas, so its bits)
-            if constexpr (SPX_CFOLD_RB > 0) {
-                // rows in blocks of RB: the finished rows' terms as RB
-                // independent chains per step (their coefficients one
-                // contiguous LDS read), then the block's own triangle
-                constexpr int RB = SPX_CFOLD_RB;
+            // one lane per column, right-looking: after step s, r_s is final
+            // and every r_t (t > s) has taken its s term (fold_rebuild_R4's
+            // fmas, so its bits)
 #pragma unroll
-                for (int t0 = 0; t0 < KW; t0 += RB) {
+            for (int s = 0; s < KW - 1; ++s) {
 #pragma unroll
-                    for (int s = 0; s < t0; ++s) {
-#pragma unroll
-                        for (int j = 0; j < RB; ++j) rq[t0 + j] = fma(NT[s][t0 + j], rq[s], rq[t0 + j]);
-                    }
-#pragma unroll
-                    for (int s = t0; s < t0 + RB - 1; ++s) {
-#pragma unroll
-                        for (int t = s + 1; t < t0 + RB; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
-                    }
-                }
-            } else {
-                // right-looking: after step s, r_s is final and every r_t
-                // (t > s) has taken its s term
-#pragma unroll
-                for (int s = 0; s < KW - 1; ++s) {
-#pragma unroll
-                    for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
-                }
+                for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
             }
             const int sl = fold_slot(lane);
 #pragma unroll
             for (int t = 0; t < KW; ++t) Rl[t][sl] = rq[t];
         }
+#endif
         lds_barrier();
         if (fst) fst[2] = rtime();
         // tiles (fold_tiles' k-step order), the first one already in flight
@@ -3441,32 +3511,55 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
             }
         }
         if (fst) fst[3] = rtime();
-        if (wave == 0 && yr == 0 && cc < S) {
-            // y_w += SY R for the group's columns (k_fold's sum, t ascending)
-            double* y = st->y_buf ? P.y1 : P.y0;
-            const int sl = fold_slot(lane);
-            double d = 0.0;
+        if (wave == 0 && yr == 0) {
+            // y_w += SY R for the group's columns (k_fold's sum, t ascending;
+            // the terms past nf dropped by a select). SY[t] is read once by
+            // lane t and handed on by readlane, so it is read before the
+            // column guard: every lane must hold its entry.
+            double syl = P.SY[lane < KW ? lane : KW - 1];
+            asm volatile("" : "+v"(syl));  // (so the read cannot sink under the guard)
+            if (cc < S) {
+                double* y = st->y_buf ? P.y1 : P.y0;
+                const int sl = fold_slot(lane);
+                double d = 0.0;
 #pragma unroll
-            for (int t = 0; t < KW; ++t)
-                if (t < nf) d = fma(P.SY[t], Rl[t][sl], d);
-            y[kc] += d;
+                for (int t = 0; t < KW; ++t) {
+                    const double v = fma(readlane_d(syl, t), Rl[t][sl], d);
+                    d = t < nf ? v : d;
+                }
+                y[kcl] += d;
+                if (fsx) fsx[7] = rtime();
+            }
         }
     }
-    if (wave == 1) {
+    if (wave == FOLD_THREADS / 64 - 1) {
         // xw += U (R b), R b = Wt[n][0..nf): the rows spread over every
-        // workgroup, one lane per row, t ascending (k_fold's)
-        const double* wb = P.Wt + P.n * KW;
+        // workgroup, one lane per row, t ascending (k_fold's); the last
+        // wave, which has tiles only when a range passes 112 rows
+        // (R b: lane t holds entry t, handed to every row by readlane)
+        double wbl = P.Wt[P.n * KW + (lane < KW ? lane : KW - 1)];
+        asm volatile("" : "+v"(wbl));  // (read by every lane, not sunk into the row loop)
         const int64_t nwg = (int64_t)gridDim.x;
         const int64_t rpw = (m + nwg - 1) / nwg;
         const int64_t r0 = (int64_t)blockIdx.x * rpw;
         const int64_t r1 = (r0 + rpw < m) ? r0 + rpw : m;
         for (int64_t i = r0 + lane; i < r1; i += 64) {
+            double u[KW];
+#pragma unroll
+            for (int t2 = 0; t2 < KW / 2; ++t2) {
+                const fdbl2 v = *reinterpret_cast<const fdbl2*>(&P.U[i * KW + 2 * t2]);
+                u[2 * t2] = v.x;
+                u[2 * t2 + 1] = v.y;
+            }
             double d = 0.0;
 #pragma unroll
-            for (int t = 0; t < KW; ++t)
-                if (t < nf) d = fma(P.U[i * KW + t], wb[t], d);
+            for (int t = 0; t < KW; ++t) {
+                const double v = fma(u[t], readlane_d(wbl, t), d);
+                d = t < nf ? v : d;
+            }
             P.xw[i] += d;
         }
+        if (fsx) fsx[6] = rtime();
     }
     __syncthreads();
     if (fst) fst[4] = rtime();
