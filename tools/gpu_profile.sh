@@ -13,7 +13,7 @@ timeout -k 10 400 python3 -u bench.py > "$OUT/bench.log" 2>&1 || exit $?
 grep '^{' "$OUT/bench.log" | tail -1 | head -c 600; echo
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --no-sharded-pricing > "$OUT/bench_under_rocprof.log" 2>&1 || exit $?
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-sharded-pricing --no-solve-to-optimum --no-steepest > "$OUT/bench_under_rocprof.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o pmc -- \
     python3 "$ROOT/tools/pmc_run.py" --k 110 > "$OUT/pmc_fetch.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o pmc -- \
