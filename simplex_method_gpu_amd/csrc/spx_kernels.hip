@@ -218,7 +218,10 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // holds after the pivot's list edit -- before the partials are reduced
     // and the base row staged -- so HBM streams during the prologue instead
     // of idling (only the end-of-list slot depends on q; it is left out)
-    constexpr bool DEEP = SPX_PRICE_DEEP && WM != 3 && BLOCK <= 512 && CH == 8;
+    // Only with y_w and the base row both staged in LDS (WM 1, the C3 / C4
+    // shape): with the base row read from L2 (WM 2, C5) it measured 4.6 %
+    // slower per pass (1,071 against 1,022 us, tools/pass_ab.py).
+    constexpr bool DEEP = SPX_PRICE_DEEP && WM == 1 && BLOCK <= 512 && CH == 8;
     dbl2 vd0[DEEP ? CH : 1], vd1[DEEP ? CH : 1];
     int64_t jdeep = -1;  // the column the deep prefetch holds (-1: none)
     // the bookkeeping's inputs for workgroup 0's thread 0, which applies them
