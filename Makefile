@@ -55,35 +55,24 @@ clean:
 
 .PHONY: all clean oracle
 
-# cache-policy variants for experiments: make variant NT=<A><BLOAD><BSTORE>, e.g. NT=101
-variant:
-	@mkdir -p $(BUILD)/v$(NT)
-	$(HIPCC) $(HIPFLAGS) -DSPX_NT_A=$(word 1,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
-	  -DSPX_NT_BLOAD=$(word 2,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
-	  -DSPX_NT_BSTORE=$(word 3,$(subst -, ,$(shell echo $(NT) | sed 's/\(.\)\(.\)\(.\)/\1-\2-\3/'))) \
-	  -c $(SRC)/spx_kernels.hip -o $(BUILD)/v$(NT)/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/v$(NT)/libsimplex.so $(BUILD)/v$(NT)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+# Experiment builds (A/B against the default: tools/pass_ab.py, tools/ab_libs.py)
+# go to $(AB), which travels to the GPU box only while it exists: `make abclean`
+# after the A/B.  (The product ships one libsimplex.so.)
+AB        := $(PKG)/_ab
 
-# in-place vs ping-pong B^-1 storage: make pingpong
-pingpong:
-	@mkdir -p $(BUILD)/pp
-	$(HIPCC) $(HIPFLAGS) -DSPX_INPLACE=0 -c $(SRC)/spx_kernels.hip -o $(BUILD)/pp/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/pp/libsimplex.so $(BUILD)/pp/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
-
-# diagnostic (timing-only, wrong results): update kernel without its tail
-diag_notail:
-	@mkdir -p $(BUILD)/notail
-	$(HIPCC) $(HIPFLAGS) -DSPX_DIAG_SKIP_TAIL=1 -c $(SRC)/spx_kernels.hip -o $(BUILD)/notail/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/notail/libsimplex.so $(BUILD)/notail/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
-
-# generic experiment build: make xlib X=name XFLAGS="-DSPX_WIN_APLDS=1"
+# generic experiment build: make xlib X=name XFLAGS="-DSPX_PRICE_DEEP=0"
 xlib:
-	@mkdir -p $(BUILD)/x$(X)
-	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_kernels.hip -o $(BUILD)/x$(X)/spx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/x$(X)/libsimplex.so $(BUILD)/x$(X)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	@mkdir -p $(AB)/x$(X)
+	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_kernels.hip -o $(AB)/x$(X)/spx_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(AB)/x$(X)/libsimplex.so $(AB)/x$(X)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
 
 # persistent-loop experiment build: make xloop X=name XFLAGS="-DSPX_LOOP_FU=4"
 xloop:
-	@mkdir -p $(BUILD)/l$(X)
-	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_loop.hip -o $(BUILD)/l$(X)/spx_loop.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(BUILD)/l$(X)/libsimplex.so $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(BUILD)/l$(X)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+	@mkdir -p $(AB)/l$(X)
+	$(HIPCC) $(HIPFLAGS) $(XFLAGS) -c $(SRC)/spx_loop.hip -o $(AB)/l$(X)/spx_loop.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(AB)/l$(X)/libsimplex.so $(BUILD)/spx_kernels.o $(BUILD)/spx_reinv.o $(BUILD)/spx_tableau.o $(AB)/l$(X)/spx_loop.o $(BUILD)/spx_api.o $(LDFLAGS)
+
+abclean:
+	rm -rf $(AB)
+
+.PHONY: xlib xloop abclean

@@ -158,6 +158,10 @@ def main():
             hs = [None] * world
             dist.all_gather_object(hs, ctx.mbox_export())
             ctx.mbox_attach(hs)
+        # the batch hipGraph is captured, instantiated and uploaded here (one
+        # rank: already by spx_create; with RCCL or mailboxes only now that
+        # they are attached), never inside a timed region
+        ctx.prepare()
         return ctx
 
     def barrier():
@@ -178,14 +182,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.tolist()
 
-    def timed_window(window, events):
-        """W warm-up pivots, untimed pivots to the next window boundary, then
-        K (rounded up to whole windows) timed pivots between barriers and
-        device syncs.  Returns the max-over-ranks time and what ran."""
+    def timed_window(window, events, spread=False):
+        """W warm-up pivots, untimed pivots to the next window boundary, one
+        more untimed whole window (so the timed passes are not the batch
+        graph's first replay), then K (rounded up to whole windows) timed
+        pivots between barriers and device syncs.  Returns the max-over-ranks
+        time and what ran; with `spread`, also the max-over-ranks times of the
+        next three windows, each timed on its own."""
         ctx = make(events, window)
         cfg = ctx.config()
         kw = cfg["window"]
         per = kw - 1 if kw else 1
+        warm = per if kw else max(cfg["graph_batch"], 1)  # one window, or one explicit batch
         steps = per * max(1, -(-args.steps // per))
         ctx.iterate(args.warmup)
         lead = 0
@@ -193,7 +201,8 @@ def main():
             ds = ctx.dispatch_stats()
             lead = (kw - ds["window_pos"]) if ds["window_pos"] < kw else 0
         info0 = ctx.info()  # (readbacks first: the lead passes run right before the timed region)
-        _, piv0 = ctx.iterate(lead)  # the next pass starts with a fold
+        ctx.iterate(lead)  # the next pass starts with a fold
+        _, piv0 = ctx.iterate(warm)  # one whole untimed window / batch: a graph replay where the library captures
         if events:
             ctx.pass_times()  # drop the warm-up's and the lead's events
             ctx.loop_times()
@@ -207,7 +216,20 @@ def main():
         dt = reduce_max([time.perf_counter() - t0])[0]
         d1 = ctx.dispatch_stats()
         delta = {k: d1[k] - d0[k] for k in ("eager_passes", "graph_launches", "graph_passes",
-                                            "persistent_launches", "persistent_passes", "folds")}
+                                            "persistent_launches", "persistent_passes", "folds", "graph_builds")}
+        windows = None
+        if spread and st == 0:
+            ts, pv = [], piv1
+            for _ in range(3):
+                barrier()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                _, p2 = ctx.iterate(warm)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+                ts[-1] = ts[-1] / max(p2 - pv, 1)
+                pv = p2
+            windows = reduce_max(ts)
         pt = lt = None
         if events:
             lt = ctx.loop_times()  # fold events (and the persistent loop's phases)
@@ -223,7 +245,8 @@ def main():
         cols = ctx.ftran_cols()
         comm = ctx.comm_info()
         ctx.close()
-        return {"cfg": cfg, "dt": dt, "pivots": piv1 - piv0, "steps": steps, "lead": lead, "dispatch": delta,
+        return {"cfg": cfg, "dt": dt, "pivots": piv1 - piv0, "steps": steps, "lead": lead + warm, "dispatch": delta,
+                "windows_s_per_pivot": windows,
                 "pt": pt, "lt": lt, "nb": 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"]),
                 "price_bytes": 0.5 * (info0["bytes_price"] + info1["bytes_price"]), "ftran_cols": cols,
                 "status": int(st), "comm": comm}
@@ -251,7 +274,7 @@ def main():
     win = args.window
     # (1) the measured run: undisturbed (no events), graph replay where the
     #     library captures, timed over whole windows
-    main_run = timed_window(win, False)
+    main_run = timed_window(win, False, spread=True)
     cfg = main_run["cfg"]
     win = cfg["window"]
     value = main_run["pivots"] / main_run["dt"] if main_run["dt"] > 0 else 0.0
@@ -378,6 +401,13 @@ def main():
                 "graph_passes": main_run["dispatch"]["graph_passes"],
                 "eager_passes": main_run["dispatch"]["eager_passes"],
                 "persistent_launches": main_run["dispatch"]["persistent_launches"],
+                "graph_builds": main_run["dispatch"]["graph_builds"],
+                "warm_up": "W pivots, then untimed pivots to the window boundary and one more untimed whole "
+                           "window (a graph replay); the batch graph was built before any of them (spx_prepare)",
+                "next_windows_it_per_s": ([1.0 / t for t in main_run["windows_s_per_pivot"]]
+                                          if main_run["windows_s_per_pivot"] else None),
+                "next_windows_spread": ((max(main_run["windows_s_per_pivot"]) / min(main_run["windows_s_per_pivot"])
+                                         - 1.0) if main_run["windows_s_per_pivot"] else None),
             },
             "roofline": {
                 "bound": "hbm",

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 6
+#define SPX_ABI_VERSION 7
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -417,9 +417,21 @@ int spx_ftran_cols(spx_ctx* ctx, int32_t* cols);
  * before the next pass when it equals [7]), [7] the window size KW (0 =
  * explicit B^-1), [8] persistent launches whose grid was found not
  * co-resident (another stream or process held CUs; the context then
- * switched to two-kernel passes and made those pivots that way). */
-#define SPX_DISPATCH_FIELDS 9
+ * switched to two-kernel passes and made those pivots that way), [9] batch
+ * hipGraphs built (captured, instantiated and uploaded; 0 or 1 per context,
+ * rebuilt once after spx_mbox_attach). */
+#define SPX_DISPATCH_FIELDS 10
 int spx_dispatch_stats(spx_ctx* ctx, int64_t out[SPX_DISPATCH_FIELDS]);
+
+/* Capture, instantiate and upload the batch hipGraph now, so that no later
+ * spx_iterate pays for it.  spx_create does this itself on one rank; with a
+ * communicator or mailboxes the graph can only be captured once they are
+ * attached (spx_attach_comm / spx_mbox_attach), and spx_iterate would
+ * otherwise build it on its first call that spans a whole batch.  A no-op
+ * when the graph exists, for eager dispatch (graph_batch < 0, timing) and for
+ * the persistent loop kernel.  If RCCL refuses the capture the context runs
+ * eager passes (spx_comm_info's graph_fallback). */
+int spx_prepare(spx_ctx* ctx);
 
 /* Host-only helpers (no device needed), shared with the device code:
  * spx_shard_range: this rank's column shard — structural columns

@@ -241,6 +241,12 @@ class Context:
         buf = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
         check(self._L.spx_mbox_attach(self._h, buf))
 
+    def prepare(self):
+        """Build (capture, instantiate, upload) the batch hipGraph now
+        (spx_prepare), e.g. right after attach_comm / mbox_attach, so no later
+        iterate() pays for it inside a timed region."""
+        check(self._L.spx_prepare(self._h))
+
     def reset(self):
         check(self._L.spx_reset(self._h))
 
@@ -406,10 +412,10 @@ class Context:
 
     def dispatch_stats(self):
         """Monotone counts of what the loop enqueued (spx_dispatch_stats)."""
-        out = (ctypes.c_int64 * 9)()
+        out = (ctypes.c_int64 * 10)()
         check(self._L.spx_dispatch_stats(self._h, out))
         keys = ("eager_passes", "graph_launches", "graph_passes", "persistent_launches", "persistent_passes",
-                "folds", "window_pos", "window", "persist_fallbacks")
+                "folds", "window_pos", "window", "persist_fallbacks", "graph_builds")
         return dict(zip(keys, list(out)))
 
     def config(self):

@@ -63,6 +63,7 @@ SIGNATURES = {
     "spx_price": (ctypes.c_int, [_p, _p, _p, _p]),
     "spx_pivot": (ctypes.c_int, [_p, _p, _p]),
     "spx_dispatch_stats": (ctypes.c_int, [_p, _p]),
+    "spx_prepare": (ctypes.c_int, [_p]),
     "spx_get_trace": (ctypes.c_int, [_p, _p, _p, _i64, _p]),
     "spx_get_weights": (ctypes.c_int, [_p, _p]),
     "spx_get_state": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p]),

@@ -141,6 +141,7 @@ struct spx_ctx {
     int64_t n_eager = 0, n_graph_launch = 0, n_graph_pass = 0, n_persist_launch = 0, n_persist_pass = 0;
     int64_t n_persist_fallback = 0;  // persistent launches found not co-resident
     int64_t n_folds = 0;
+    int64_t n_graph_builds = 0;  // batch graphs captured + instantiated + uploaded
     int graph_folds = 0;     // folds inside one captured batch
     bool capturing = false;  // build_graph: passes are recorded, not run
 
@@ -717,6 +718,7 @@ int build_graph(spx_ctx* x) {
     if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
     x->graph = g;
     if (ei != hipSuccess) return fail(SPX_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+    ++x->n_graph_builds;
     // the first launch of a fresh graph pays its upload (measured 13 ms for a
     // 63-node graph): do it here, not inside somebody's timed loop
     HIP_TRY(hipGraphUpload(x->graph_exec, x->stream));
@@ -1045,25 +1047,34 @@ int set_slack_flags(spx_ctx* x) {
     x->P.slack_unit = (ident && !env_on("SPX_DENSE_SLACKS")) ? 1 : 0;
     if (x->bc_want && ident) {  // compact FTRAN operand (do_reset initialises it)
         Params& P = x->P;
-        // 2 x m x L more doubles (2 x 2.1 GB at C5; the compact fold writes
-        // the other buffer, spx_device.h): when they do not fit, the dense
-        // B_w stream that fit before is kept (every kernel tests P.bc)
-        void* d[2] = {nullptr, nullptr};
-        for (int k = 0; k < 2; ++k) {
-            if (hipMalloc(&d[k], (size_t)(m * x->L) * sizeof(double)) != hipSuccess) {
+        // m x L more doubles (2.1 GB at C5), and a second buffer of that
+        // shape for the compact fold (it writes the other one, spx_device.h).
+        // No room for the first: the dense B_w stream is kept (every kernel
+        // tests P.bc).  No room for the second: compact FTRAN with the dense
+        // fold plus the gather (k_fold + k_bc_gather, bc_n[2] stays 0).
+        const size_t bytes = (size_t)(m * x->L) * sizeof(double);
+        void* d0 = nullptr;
+        if (hipMalloc(&d0, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            x->bc_want = false;
+            return SPX_OK;
+        }
+        x->allocs.push_back(d0);
+        HIP_TRY(hipMemsetAsync(d0, 0, bytes, x->stream));
+        P.bc = static_cast<double*>(d0);
+        P.bc1 = nullptr;
+        P.cfold = 0;
+        if (!env_on("SPX_DENSE_FOLD")) {
+            void* d1 = nullptr;
+            if (hipMalloc(&d1, bytes) == hipSuccess) {
+                x->allocs.push_back(d1);
+                HIP_TRY(hipMemsetAsync(d1, 0, bytes, x->stream));
+                P.bc1 = static_cast<double*>(d1);
+                P.cfold = 1;
+            } else {
                 (void)hipGetLastError();
-                if (k == 1) (void)hipFree(d[0]);
-                x->bc_want = false;
-                return SPX_OK;
             }
         }
-        for (int k = 0; k < 2; ++k) {
-            x->allocs.push_back(d[k]);
-            HIP_TRY(hipMemsetAsync(d[k], 0, (size_t)(m * x->L) * sizeof(double), x->stream));
-        }
-        P.bc = static_cast<double*>(d[0]);
-        P.bc1 = static_cast<double*>(d[1]);
-        P.cfold = env_on("SPX_DENSE_FOLD") ? 0 : 1;
         SPX_TRY(x->alloc(&P.rlist, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rmap, (size_t)x->L));
         SPX_TRY(x->alloc(&P.rleft, (size_t)x->L));
@@ -1649,7 +1660,14 @@ int spx_dispatch_stats(spx_ctx* x, int64_t out[SPX_DISPATCH_FIELDS]) {
     out[6] = x->P.win ? x->nw : 0;
     out[7] = x->P.win;
     out[8] = x->n_persist_fallback;
+    out[9] = x->n_graph_builds;
     return SPX_OK;
+}
+
+int spx_prepare(spx_ctx* x) {
+    if (!x) return fail(SPX_ERR_ARG, "ctx is NULL");
+    if (x->persist) return SPX_OK;  // one launch per window: nothing to capture
+    return build_graph(x);
 }
 
 int spx_pass_times(spx_ctx* x, double out[3], int64_t* passes) {

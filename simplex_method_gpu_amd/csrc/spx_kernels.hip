@@ -50,15 +50,6 @@ namespace spx {
 #ifndef SPX_PRICE_CH
 #define SPX_PRICE_CH 8  // chunks of a column's start prefetched (8-wave workgroups)
 #endif
-#ifndef SPX_CFOLD_T
-#define SPX_CFOLD_T 1  // k_cfold: R rebuilt one lane per row, 8 columns per wave (0: one lane per column)
-#endif
-#ifndef SPX_CFOLD_EXEC
-#define SPX_CFOLD_EXEC 1  // k_cfold (SPX_CFOLD_T): lanes t <= s masked per step by exec (0: a select per fma)
-#endif
-#ifndef SPX_MERGE1
-#define SPX_MERGE1 0  // deferred tail: one wave merges the wave partials and hands the result on (A/B)
-#endif
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
@@ -85,9 +76,6 @@ constexpr int BC_PF = SPX_BC_PF;
 constexpr int BC_PF2 = SPX_BC_PF2;  // chunks requested once S is known (up to 512 columns)
 constexpr int BC_APC = 8192;  // A_p gathered onto the list in LDS blocks of this many columns
 constexpr int BC_RL = 2;
-#ifndef SPX_FTRAN_TRIM
-#define SPX_FTRAN_TRIM 0  // k_ftran_bc: compact-row chunk 0 and U rows read only where used (A/B)
-#endif
 
 // Diagnostic phase stamps: slot[0] = earliest workgroup start of the current
 // launch, slot[1] += (last-workgroup ticket - start), slot[2] += tail duration.
@@ -221,7 +209,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // Only with y_w and the base row both staged in LDS (WM 1, the C3 / C4
     // shape): with the base row read from L2 (WM 2, C5) it measured 4.6 %
     // slower per pass (1,071 against 1,022 us, tools/pass_ab.py).
-    constexpr bool DEEP = SPX_PRICE_DEEP && WM == 1 && BLOCK <= 512 && CH == 8;
+    // (only run_pipe consumes vd0 / vd1, so DEEP needs the pipelined loop)
+    constexpr bool DEEP = SPX_PRICE_DEEP && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8;
     dbl2 vd0[DEEP ? CH : 1], vd1[DEEP ? CH : 1];
     int64_t jdeep = -1;  // the column the deep prefetch holds (-1: none)
     // the bookkeeping's inputs for workgroup 0's thread 0, which applies them
@@ -1125,22 +1114,7 @@ __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, 
     const UpdPartial o = wave_reduce_partial(w);
     if (lane == 0) red[wave] = o;
     lds_barrier();
-    if constexpr (PLAIN && SPX_MERGE1) {
-        // wave 0 merges (the same order) and hands the result to the other
-        // waves through one more LDS slot: one wave reads the WAVES partials
-        // instead of every wave (the callers' arrays hold WAVES + 1)
-        if (wave == 0) {
-            UpdPartial r[WAVES];
-#pragma unroll
-            for (int k = 0; k < WAVES; ++k) r[k] = red[k];
-            UpdPartial t = r[0];
-#pragma unroll
-            for (int k = 1; k < WAVES; ++k) upd_merge_sel(t, r[k]);
-            if (lane == 0) red[WAVES] = t;
-        }
-        lds_barrier();
-        return red[WAVES];
-    } else if constexpr (PLAIN) {
+    if constexpr (PLAIN) {
         // the deferred tail (k_price's prologue, k_apply_tail): every wave
         // partial requested before a branch-free merge, and no closing
         // barrier (the callers pass an LDS array of their own).  (In the
@@ -1747,7 +1721,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 #pragma unroll
                 for (int u = 0; u < R; ++u) {
                     if (u < nvalid) {
-                        const dbl2* brow = reinterpret_cast<const dbl2*>(P.bc) + (lr0 + u) * (int64_t)(P.bc_n[1] >> 1);
+                        // the active buffer (bc_n[2]), as the prefetches above read it
+                        const dbl2* brow = reinterpret_cast<const dbl2*>(bc_buf(P, P.bc_n[2])) +
+                                           (lr0 + u) * (int64_t)(P.bc_n[1] >> 1);
                         auto take = [&](dbl2 v, int k2) {
                             const dbl2 w = apc2[k2 - kb];
                             if (2 * k2 < S) a[u] = fma(v.x, w.x, a[u]);
@@ -2010,9 +1986,6 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     else lds_barrier();
     if (!*s_last) return;
     const unsigned long long t_tail = slot ? rtime() : 0;
-#ifdef SPX_DIAG_SKIP_TAIL  // timing-only build: pivots stop after the first pass
-    if (true) return;
-#endif
     if constexpr (RS)
         update_tail_rs<BLOCK>(P, st, it, par, a_prev, smem, gridDim.x);
     else
@@ -2088,7 +2061,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
         cbv[r] = P.c_B[icl[r]];
         xb0[r] = P.x_b[icl[r]];
         bix[r] = P.b_ixs[icl[r]];
-        if (!SPX_FTRAN_TRIM) urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
+        urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
     }
     const double sxw_w = P.Wt[P.n * KW + (lane < KW ? lane : 0)];
     struct {
@@ -2119,18 +2092,13 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
 #pragma unroll
         for (int t = 0; t < NCH; ++t) {
             const int k2 = lane + 64 * t;
-            const int kk = (t == 0 && !SPX_FTRAN_TRIM) ? (k2 < L2 ? k2 : (int)L2 - 1)
-                                                       : ((2 * k2 < Sbc && k2 < L2) ? k2 : (t == 0 ? 0 : lane));
+            const int kk = t == 0 ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
             pf[r][t] = brow[r][kk];
         }
     }
     const int64_t qp = Sv.q;
     const bool pend = Sv.nw > 0;
     const int tau = Sv.nw - 1;
-    if (SPX_FTRAN_TRIM) {  // U rows: the pivots of the window only (lanes < tau)
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) urow[r] = P.U[icl[r] * KW + (lane < tau ? lane : 0)];
-    }
     const double sxw_u = P.U[(pend ? qp : 0) * KW + (lane < KW ? lane : 0)];
     const double sx_x = P.xw[pend ? qp : 0];
     __builtin_amdgcn_sched_barrier(0);
@@ -3340,7 +3308,6 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         // and pinned below, so the compiler cannot turn it into a guarded
         // load waited for on the spot)
         int kcl = P.rlist[cc < L ? cc : L - 1];
-#if SPX_CFOLD_T
         // R, one lane per row t and eight columns per wave (columns
         // c0 + 8 wave + j): lane t holds N[t][s] = Urows[t][s] (0 unless
         // s < t < nf) and r_t of each column; step s hands r_s (final after
@@ -3370,19 +3337,6 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
             const int k = (unsigned)kl[j] < (unsigned)L ? kl[j] : 0;
             rt[j] = P.Qrows[(int64_t)tl * L + k];
         }
-#else
-        // operands of R (this lane's column c0 + lane) and the coefficients
-        const int kc = cc < S ? kcl : 0;
-        double rq[KW];
-#pragma unroll
-        for (int t = 0; t < KW; ++t) rq[t] = (t < nf && cc < S && wave == 0) ? P.Qrows[(int64_t)t * L + kc] : 0.0;
-        FoldRPre<KW> rpre;
-#pragma unroll
-        for (int j = 0; j < FoldRPre<KW>::NPT; ++j) {
-            const int k = tid + j * FOLD_THREADS;
-            rpre.n[j] = P.Urows[k < KW * KW ? k : KW * KW - 1];
-        }
-#endif
         // the list entries of this lane's tile columns (unit entries past S0)
         int rk[4];
 #pragma unroll
@@ -3396,7 +3350,6 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
         const int64_t step = 16 * (int64_t)(FOLD_THREADS / 64);
         int64_t r0 = i0 + 16 * wave;
         FoldTilePre<KW> cur;
-#if SPX_CFOLD_T
         // (unconditional: rows clamped into the range, a branch here made
         // the compiler wait for everything before the rebuild)
         cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
@@ -3414,22 +3367,13 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
 #pragma unroll
             for (int s = 0; s < KW - 1; ++s) {
                 const double co = NT[s][tl];
-                if constexpr (SPX_CFOLD_EXEC) {
-                    // one exec mask per step for the wave's columns
-                    double rs[CPW];
+                // one exec mask per step for the wave's columns
+                double rs[CPW];
 #pragma unroll
-                    for (int j = 0; j < CPW; ++j) rs[j] = readlane_d(rt[j], s);
-                    if (lane > s) {
+                for (int j = 0; j < CPW; ++j) rs[j] = readlane_d(rt[j], s);
+                if (lane > s) {
 #pragma unroll
-                        for (int j = 0; j < CPW; ++j) rt[j] = fma(co, rs[j], rt[j]);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < CPW; ++j) {
-                        const double rs = readlane_d(rt[j], s);
-                        const double v = fma(co, rs, rt[j]);
-                        rt[j] = lane > s ? v : rt[j];
-                    }
+                    for (int j = 0; j < CPW; ++j) rt[j] = fma(co, rs[j], rt[j]);
                 }
             }
         } else {
@@ -3440,25 +3384,6 @@ __global__ __launch_bounds__(FOLD_THREADS) void k_cfold(Params P, int min_nw) {
 #pragma unroll
             for (int j = 0; j < CPW; ++j) Rl[lane][fold_slot(CPW * wave + j)] = rt[j];
         }
-#else
-        if (r0 < i1) cfold_tile_issue<KW>(Bo, ldo, S0, P.U, c0, r0, i1, cur);
-        fold_stage_N_pre<KW>(rpre, nf, NT);
-        lds_barrier();
-        if (fst) fst[1] = rtime();
-        if (wave == 0) {
-            // one lane per column, right-looking: after step s, r_s is final
-            // and every r_t (t > s) has taken its s term (fold_rebuild_R4's
-            // fmas, so its bits)
-#pragma unroll
-            for (int s = 0; s < KW - 1; ++s) {
-#pragma unroll
-                for (int t = s + 1; t < KW; ++t) rq[t] = fma(NT[s][t], rq[s], rq[t]);
-            }
-            const int sl = fold_slot(lane);
-#pragma unroll
-            for (int t = 0; t < KW; ++t) Rl[t][sl] = rq[t];
-        }
-#endif
         lds_barrier();
         if (fst) fst[2] = rtime();
         // tiles (fold_tiles' k-step order), the first one already in flight

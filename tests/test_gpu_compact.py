@@ -259,3 +259,39 @@ def test_compact_fold_persistent_and_reinversion(spx, oracle):
     A, b, c = oracle.generate(kw["m"], kw["n"], kw["seed"])
     o = oracle.solve(A, b, c, eps=1e-7)
     assert ra.status == spx.SolveStatus.OptimumFound and abs(ra.z - o.z) <= 1e-9 * abs(o.z)
+
+
+@pytest.mark.parametrize("kw,env", [(dict(update_rows=2), {}), (dict(), dict(SPX_FTRAN_BC_ENTRY="0"))],
+                         ids=["rows2", "k_update-bc"])
+def test_compact_fold_wide_list_k_update(spx, kw, env):
+    """k_update<..., BC> (update_rows > 1, or SPX_FTRAN_BC_ENTRY=0) with a
+    column list past BC_PF2 chunks (S > 512) after odd and even numbers of
+    compact folds: every chunk of a row comes from the active operand buffer
+    at its pitch (the chunks past the prefetch were read
+    from buffer 0), so the bits are those of the dense fold plus the gather
+    (SPX_DENSE_FOLD=1, one buffer)."""
+    m, n, seed = 2048, 8192, 7
+    basis = np.arange(n - m, n, dtype=np.int64)
+    basis[:600] = np.arange(600)  # structural columns 0..599 in rows 0..599: S = 600
+    outs = []
+    for dense in ("0", "1"):
+        with _env(SPX_DENSE_FOLD=dense, **env):
+            with spx.Context(m=m, n=n, seed=seed, window=16, persist=False, trace=4096, **kw) as ctx:
+                try:
+                    ctx.set_basis(basis)
+                except spx.SimplexError:
+                    pytest.skip("that basis is singular for this seed")
+                assert ctx.ftran_cols() == 600
+                outs.append([])
+                for k in (15, 15, 15, 52):  # folds before each: 0, 1, 2, 3 (odd and even buffers)
+                    st, piv = ctx.iterate(k)
+                    s = ctx.state(binv=True)
+                    outs[-1].append((piv, s))
+                outs[-1].append(ctx.trace())
+    a, b = outs
+    assert a[-1][0].size > 60
+    assert np.array_equal(a[-1][0], b[-1][0]) and np.array_equal(a[-1][1], b[-1][1])
+    for (pa, sa), (pb, sb) in zip(a[:-1], b[:-1]):
+        assert pa == pb
+        for key in ("b_ixs", "x_b", "y", "binv"):
+            assert np.array_equal(sa[key], sb[key]), key
