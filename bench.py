@@ -192,8 +192,10 @@ def main():
         ctx = make(events, window)
         cfg = ctx.config()
         kw = cfg["window"]
-        per = kw - 1 if kw else 1
-        warm = per if kw else max(cfg["graph_batch"], 1)  # one window, or one explicit batch
+        # whole windows (eta window), or whole captured batches of passes
+        # (explicit B^-1: the timed region replays graphs, as the window's does)
+        per = kw - 1 if kw else max(cfg["graph_batch"], 1)
+        warm = per
         steps = per * max(1, -(-args.steps // per))
         ctx.iterate(args.warmup)
         lead = 0
@@ -394,7 +396,9 @@ def main():
             },
             "timed_region": {
                 "pivots": main_run["pivots"],
-                "steps_rounding": f"K rounded up to whole windows of {win - 1} pivots" if win else "none",
+                "steps_rounding": (f"K rounded up to whole windows of {win - 1} pivots" if win else
+                                   f"K rounded up to whole captured batches of {cfg['graph_batch']} passes"
+                                   if cfg["graph_batch"] > 0 else "none"),
                 "untimed_pivots_before": args.warmup + main_run["lead"],
                 "folds": main_run["dispatch"]["folds"],
                 "graph_launches": main_run["dispatch"]["graph_launches"],

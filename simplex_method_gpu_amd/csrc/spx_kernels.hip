@@ -184,7 +184,36 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // status word (index clamped into the list; validated against nb_count)
     int64_t j0 = P.nb_list[idx0 < P.n ? idx0 : P.n - 1];
     const unsigned long long t_pw0 = P.stamps ? rtime() : 0ull;
-    const DevState S = st_snapshot(st);
+    // Deferred tail: the record and this thread's partial(s) are requested at
+    // entry beside the column and the state -- unconditionally (clamped
+    // slot), so no test of the record or the state sits between them: a
+    // branch there made the compiler wait for the state, then for the
+    // record, before the partials were even requested (three round trips)
+    // (a record of zeros when there is none: a branch around these loads
+    // moved the record's uniform fields into SGPRs inside it, i.e. waited)
+    // Only the compact window passes defer the tail (the explicit form and the
+    // tableau never do: no record, no partials, no loads)
+    constexpr bool PAIR = BLOCK == 256;  // (two partials of the 512-thread shape per thread)
+    constexpr bool DT = WM != 0 && WM != 3;
+    TailRec R{};
+    if constexpr (DT) R = *(P.defer_tail ? P.trec : reinterpret_cast<const TailRec*>(P.zeros));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int SW = (int)(sizeof(DevState) / 16);
+    u32x4 sw[SW];  // the state as raw words (st_snapshot's loads)
+#pragma unroll
+    for (int i = 0; i < SW; ++i) sw[i] = reinterpret_cast<const u32x4*>(st)[i];
+    UpdPartial w0 = upd_empty(), w1 = upd_empty();
+    if constexpr (DT) {
+        const int tp = P.tail_parts > 0 ? P.tail_parts : 1;
+        w0 = upd_fetch<true>(P, tid < tp ? tid : tp - 1);
+        if constexpr (PAIR) w1 = upd_fetch<true>(P, tid + BLOCK < tp ? tid + BLOCK : tp - 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // (every state word held until here: a dead word's register, reused
+    // early, made the partials' loads wait for the state)
+#pragma unroll
+    for (int i = 0; i < SW; ++i) asm volatile("" ::"v"(sw[i]));
+    const DevState S = __builtin_bit_cast(DevState, sw);
     // the fields the pass prices with (fresh: derived from the deferred tail;
     // kept as scalars -- assigning into the snapshot put it in scratch)
     int64_t s_iter = S.iter, s_q = S.q, s_leave = S.leave;
@@ -221,33 +250,37 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
 #if defined(SPX_DIAG_FETCH_STAMP) || defined(SPX_DIAG_MERGE_STAMP)
     unsigned long long t_fetch_all = 0;
 #endif
-    if (P.defer_tail) {
-        // this thread's partial is requested beside the record, not behind
-        // its test (that was a second round trip)
-        // 256-thread workgroups hold two threads' partials of the FTRAN
-        // tail's 512-thread shape (reduce_partial_pair: the same bits)
-        constexpr bool PAIR = BLOCK == 256;
-        const TailRec R = *P.trec;  // (first: the deep prefetch waits for it alone)
-        UpdPartial w0 = tid < P.tail_parts ? upd_fetch<true>(P, tid) : upd_empty();
-        UpdPartial w1 = upd_empty();
-        if constexpr (PAIR) {
-            if (tid + BLOCK < P.tail_parts) w1 = upd_fetch<true>(P, tid + BLOCK);
-        }
+    if (DT && P.defer_tail) {
         fresh = R.fresh != 0;
         if constexpr (DEEP) {
             // slots below cnt0 hold the same column before and after the
-            // list edit, except p's slot R.kp, which takes the last entry
+            // list edit, except p's slot R.kp, which takes the last entry.
+            // The loads are unconditional (column and chunk clamped): behind
+            // a branch, the compiler's waits for the partials below covered
+            // these 16 loads too (the wait counts of the two paths merge)
             const int64_t L2d = P.L >> 1;
             const int32_t cnt0 = fresh ? (R.kp >= 0 ? R.cnt - 1 : R.cnt) : S.nb_count;
-            if (idx0 < cnt0 && (L2d & 511) == 0 && L2d >= 2 * CH * 64) {
-                const int64_t jd = (fresh && R.kp >= 0 && idx0 == R.kp) ? (int64_t)R.last : j0;
-                const dbl2* cd = reinterpret_cast<const dbl2*>(P.A + jd * P.L);
+            const bool dv = idx0 < cnt0 && (L2d & 511) == 0 && L2d >= 2 * CH * 64;
+            int64_t jd = (fresh && R.kp >= 0 && idx0 == R.kp) ? (int64_t)R.last : j0;
+            jd = (uint64_t)jd < (uint64_t)P.n ? jd : 0;
+            const dbl2* cd = reinterpret_cast<const dbl2*>(P.A + jd * P.L);
 #pragma unroll
-                for (int u = 0; u < CH; ++u) vd0[u] = ld2<SPX_NT_A>(&cd[lane + u * 64]);
-#pragma unroll
-                for (int u = 0; u < CH; ++u) vd1[u] = ld2<SPX_NT_A>(&cd[CH * 64 + lane + u * 64]);
-                jdeep = jd;
+            for (int u = 0; u < CH; ++u) {
+                const int64_t k = lane + u * 64;
+                vd0[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
             }
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int64_t k = CH * 64 + lane + u * 64;
+                vd1[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
+            }
+            jdeep = dv ? jd : -1;
+        }
+        // slots past the FTRAN pass's partials: empty (after the deep loads'
+        // issue: the selects wait for the partials)
+        if (tid >= P.tail_parts) w0 = upd_empty();
+        if constexpr (PAIR) {
+            if (tid + BLOCK >= P.tail_parts) w1 = upd_empty();
         }
         if (fresh) {
             __shared__ UpdPartial s_ured[(PAIR ? 2 * WAVES : WAVES) + 1];

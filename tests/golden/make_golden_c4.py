@@ -1,0 +1,44 @@
+"""Independent optimum for BASELINE config C4 (m=4096, n=131072, seed 0), run in
+the build container: scipy HiGHS dual simplex (the solver standing in for
+GLPK, solver_glpk.cpp:23; libglpk is absent in this image) on the seeded LP of
+SURVEY.md §8(d).  Writes ``tests/golden/highs_c4.json`` (the optimum, the
+basic set, HiGHS's wall time and the process's peak resident memory).  Data
+only; the GPU tests solve C4 to optimality and compare with it
+(tests/test_gpu_c4_optimum.py).
+
+    python tests/golden/make_golden_c4.py [m n seed]
+"""
+from __future__ import annotations
+
+import json
+import os
+import resource
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import oracle  # noqa: E402
+from make_golden import highs_optimum  # noqa: E402
+
+
+def main():
+    m, n, seed = (int(v) for v in sys.argv[1:4]) if len(sys.argv) >= 4 else (4096, 131072, 0)
+    A, b, c = oracle.generate(m, n, seed)
+    t0 = time.time()
+    z, basis, _ = highs_optimum(A, b, c)
+    t1 = time.time()
+    rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20
+    print(f"highs z={z:.15g} ({t1 - t0:.1f} s, peak RSS {rss_gb:.1f} GB)", flush=True)
+    out = {"generator": "SURVEY.md §8(d) splitmix64; A=[U|I], b=(n-m)/4*U(1,2), c=U(0,1)|0",
+           "solver": "scipy %s linprog(method='highs-ds')" % __import__("scipy").__version__,
+           "m": m, "n": n, "seed": seed, "highs_z": z, "highs_basis": basis,
+           "highs_seconds": t1 - t0, "peak_rss_gb": rss_gb}
+    name = "highs_c4.json" if (m, n, seed) == (4096, 131072, 0) else f"highs_{m}x{n}_{seed}.json"
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(out, f)
+
+
+if __name__ == "__main__":
+    main()
