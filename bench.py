@@ -226,7 +226,7 @@ def main():
                 barrier()
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
-                _, p2 = ctx.iterate(warm)
+                _, p2 = ctx.iterate(steps)
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t1)
                 ts[-1] = ts[-1] / max(p2 - pv, 1)

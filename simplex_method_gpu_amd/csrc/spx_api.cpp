@@ -1092,7 +1092,7 @@ int set_slack_flags(spx_ctx* x) {
     const UpdateCfg& uc = x->ucfg;
     const bool tail_ok = x->defer_ok || (x->use_comm && x->P.win && !x->P.split_tail && !x->P.row_shard &&
                                          !(x->opts.flags & SPX_FLAG_PRICE_TAIL));
-    if (x->P.bc && tail_ok && !x->persist && !x->P.steep && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
+    if (x->P.bc && tail_ok && !x->persist && !x->P.tab && uc.bc_entry && uc.rows == 1 &&
         uc.block == 512 && (x->pcfg.block == 512 || x->pcfg.block == 256) && !env_off("SPX_DEFER_TAIL")) {
         SPX_TRY(x->alloc(&x->P.trec, 1));
         HIP_TRY(hipMemset(x->P.trec, 0, sizeof(TailRec)));

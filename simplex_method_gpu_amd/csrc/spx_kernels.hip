@@ -1196,8 +1196,7 @@ __device__ __forceinline__ UpdPartial reduce_partial_pair(const UpdPartial& wa, 
 template <int BLOCK, bool PLAIN>
 __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag,
                                              bool* timed_out) {
-    constexpr int WAVES = BLOCK / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     UpdPartial w = upd_empty();
     if (tag) {  // tagged hand-off: poll, then clear the consumed slots
         bool ok = true;
@@ -3686,13 +3685,31 @@ hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n
 // columns (the compact list, or all of B_w) | U | alpha], per row block in
 // ascending row order, then over the blocks in ascending order.
 // ---------------------------------------------------------------------------
-constexpr int SE_RB = 64;  // rows per k_se_part workgroup
+// Round 5: both kernels latency-bound no more (C3 steepest pass: the two took
+// about 28 us): k_se_part's threads request a 16-row block of their column at
+// once, and k_se_fin sums the row-block partials of 64 columns per workgroup
+// with 16 slices of threads (coalesced, 16 loads in flight per thread), then
+// the slices in ascending order.
+constexpr int SE_RB = 16;     // rows per k_se_part workgroup
+constexpr int SE_SLICES = 16;  // k_se_fin: partial slices per column (1024 threads = 64 columns x 16)
 
+// The pending pivot (its alpha parity and the window position): from the
+// state, or -- when the FTRAN pass deferred its tail (TailRec) -- from the
+// record, as the next k_price derives it
 __device__ __forceinline__ bool se_pending(const Params& P, int& nw, const double*& al) {
     const DevState* st = P.st;
-    if (st->status != ST_RUNNING || st->iter >= st->limit) return false;
-    nw = st->nw;
-    al = (st->iter & 1) ? P.alpha1 : P.alpha0;  // alpha of the pending pivot
+    int64_t iter = st->iter;
+    int32_t nwv = st->nw;
+    if (P.trec) {
+        const TailRec R = *P.trec;
+        if (R.fresh) {
+            iter = R.it + 1;
+            nwv = R.nw + 1;
+        }
+    }
+    if (st->status != ST_RUNNING || iter >= st->limit) return false;
+    nw = nwv;
+    al = (iter & 1) ? P.alpha1 : P.alpha0;  // alpha of the pending pivot
     return nw > 0;
 }
 
@@ -3713,21 +3730,34 @@ __global__ __launch_bounds__(256) void k_se_part(Params P) {
     const int64_t ldm = P.bc ? (int64_t)P.bc_n[1] : L;  // row pitch (compact: bc_pitch)
     double* out = P.se_part + (int64_t)blockIdx.x * (L + KW + 1);
     for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
-        double acc = 0.0;
+        // the block's rows of column c, requested together (rows clamped;
+        // the sum takes rows < nr in ascending order)
+        const double* src;
+        int64_t ld;
         if (c < S) {
-            for (int r = 0; r < nr; ++r) acc = fma(Mw[(i0 + r) * ldm + c], sa[r], acc);
+            src = Mw + c;
+            ld = ldm;
         } else if (c < S + KW) {
             const int sc = c - S;
-            if (sc < tau)
-                for (int r = 0; r < nr; ++r) acc = fma(P.U[(i0 + r) * KW + sc], sa[r], acc);
+            src = P.U + (sc < tau ? sc : 0);
+            ld = KW;
         } else {
-            for (int r = 0; r < nr; ++r) acc = fma(sa[r], sa[r], acc);
+            src = al;
+            ld = 1;
         }
+        double v[SE_RB];
+#pragma unroll
+        for (int r = 0; r < SE_RB; ++r) v[r] = src[(i0 + (r < nr ? r : nr - 1)) * ld];
+        double acc = 0.0;
+        const bool live = c < S || c >= S + KW || c - S < tau;
+#pragma unroll
+        for (int r = 0; r < SE_RB; ++r)
+            if (r < nr && live) acc = fma(c < S + KW ? v[r] : sa[r], sa[r], acc);
         out[c] = acc;
     }
 }
 
-__global__ __launch_bounds__(256) void k_se_fin(Params P) {
+__global__ __launch_bounds__(1024) void k_se_fin(Params P) {
     int nw;
     const double* al;
     if (!se_pending(P, nw, al)) return;
@@ -3736,18 +3766,39 @@ __global__ __launch_bounds__(256) void k_se_fin(Params P) {
     const int S = P.bc ? P.bc_n[0] : (int)m;
     const int ncols = S + KW + 1;
     const int64_t stride = L + KW + 1;
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t c = t0; c < ncols; c += nt) {
-        double v = 0.0;
-        for (int g = 0; g < P.se_parts; ++g) v += P.se_part[g * stride + c];
-        if (c < S) P.se_v[P.bc ? (int64_t)P.rlist[c] : c] = v;
-        else if (c < S + KW) P.se_cg[c - S] = v;
-        else P.se_cg[KW] = 1.0 + v;
+    const int tid = threadIdx.x, cl = tid & 63, sl = tid >> 6;  // column in the group, slice
+    const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+    __shared__ double red[SE_SLICES][64];
+    // slice sl sums the partials g = sl, sl + 16, ... (ascending), 16 at a time
+    double v = 0.0;
+    const int64_t cc = c < ncols ? c : 0;
+    const int gend = (int64_t)blockIdx.x * 64 < ncols ? P.se_parts : 0;  // (groups past the columns: nothing)
+    for (int g0 = sl; g0 < gend; g0 += SE_SLICES * 16) {
+        double t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int g = g0 + k * SE_SLICES;
+            t[k] = P.se_part[(int64_t)(g < P.se_parts ? g : 0) * stride + cc];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (g0 + k * SE_SLICES < P.se_parts) v += t[k];
     }
-    if (P.bc)  // the unit columns of B_w: (B_w^T alpha)_k = alpha_k
+    red[sl][cl] = v;
+    __syncthreads();
+    if (sl == 0 && c < ncols) {
+        double w = red[0][cl];
+#pragma unroll
+        for (int k = 1; k < SE_SLICES; ++k) w += red[k][cl];
+        if (c < S) P.se_v[P.bc ? (int64_t)P.rlist[c] : c] = w;
+        else if (c < S + KW) P.se_cg[c - S] = w;
+        else P.se_cg[KW] = 1.0 + w;
+    }
+    if (P.bc) {  // the unit columns of B_w: (B_w^T alpha)_k = alpha_k
+        const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + tid, nt = (int64_t)gridDim.x * blockDim.x;
         for (int64_t k = t0; k < m; k += nt)
             if (P.rmap[k] < 0) P.se_v[k] = al[k];
+    }
 }
 
 // gamma_j = 1 + ||A_j||^2 for every column (the slack basis B = I), one wave
@@ -3774,7 +3825,8 @@ hipError_t launch_se_init(const Params& P, hipStream_t s) {
 hipError_t launch_se_prep(const Params& P, hipStream_t s) {
     if (!P.steep) return hipSuccess;
     hipLaunchKernelGGL(k_se_part, dim3((unsigned)P.se_parts), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_se_fin, dim3(grid_for(P.L + P.win + 1, 256)), dim3(256), 0, s, P);
+    // 64 columns per workgroup (the columns in use, S + KW + 1, are at most L + KW + 1)
+    hipLaunchKernelGGL(k_se_fin, dim3((unsigned)((P.L + P.win + 1 + 63) / 64)), dim3(1024), 0, s, P);
     return hipGetLastError();
 }
 

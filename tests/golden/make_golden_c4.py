@@ -7,6 +7,9 @@ only; the GPU tests solve C4 to optimality and compare with it
 (tests/test_gpu_c4_optimum.py).
 
     python tests/golden/make_golden_c4.py [m n seed]
+
+The basis is read from x as make_golden.highs_optimum does (the m largest
+entries); the LP is the same as there.
 """
 from __future__ import annotations
 
@@ -19,15 +22,37 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import numpy as np  # noqa: E402
+import scipy.sparse as sp  # noqa: E402
+from scipy.optimize import linprog  # noqa: E402
+
 import oracle  # noqa: E402
-from make_golden import highs_optimum  # noqa: E402
 
 
 def main():
     m, n, seed = (int(v) for v in sys.argv[1:4]) if len(sys.argv) >= 4 else (4096, 131072, 0)
     A, b, c = oracle.generate(m, n, seed)
+    # A = [U | I] handed over as CSC (the structural columns dense, the slack
+    # columns unit), built without a dense transpose: the dense path ran out
+    # of the container's memory inside HiGHS (std::bad_alloc at 52 GB)
+    ns = n - m
+    data = np.empty(ns * m + m)
+    data[: ns * m] = A[:ns].reshape(-1)
+    data[ns * m:] = 1.0
+    del A
+    indices = np.empty(ns * m + m, dtype=np.int32)
+    indices[: ns * m].reshape(ns, m)[:] = np.arange(m, dtype=np.int32)
+    indices[ns * m:] = np.arange(m, dtype=np.int32)
+    indptr = np.concatenate([np.arange(ns + 1, dtype=np.int64) * m, ns * m + 1 + np.arange(m, dtype=np.int64)])
+    Acsc = sp.csc_array((data, indices, indptr), shape=(m, n))
+    del data, indices
     t0 = time.time()
-    z, basis, _ = highs_optimum(A, b, c)
+    res = linprog(-c, A_eq=Acsc, b_eq=b, bounds=(0, None), method="highs-ds",
+                  options={"primal_feasibility_tolerance": 1e-10, "dual_feasibility_tolerance": 1e-10,
+                           "presolve": False})  # (presolve copies the LP: no room for it here)
+    assert res.status == 0, res.message
+    z = float(-res.fun)
+    basis = sorted(int(j) for j in np.argsort(-res.x)[:m])
     t1 = time.time()
     rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20
     print(f"highs z={z:.15g} ({t1 - t0:.1f} s, peak RSS {rss_gb:.1f} GB)", flush=True)

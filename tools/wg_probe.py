@@ -22,8 +22,10 @@ ap.add_argument("--samples", type=int, default=12)
 ap.add_argument("--step", type=int, default=7)
 ap.add_argument("--warm", type=int, default=70)
 ap.add_argument("--eager", action="store_true", help="one launch pair per iterate() call")
+ap.add_argument("--pricing", type=int, default=0, help="0 Dantzig, 1 Devex, 2 steepest edge")
 a = ap.parse_args()
 kw = dict(graph_batch=-1) if a.eager else {}
+kw["pricing"] = a.pricing
 S = {}
 
 
@@ -80,6 +82,6 @@ out["price_end_p10_p50_p90_max"] = [round(float(np.percentile(E, q)), 2) for q i
 me = E.mean(0)
 out["price_slowest_wg"] = [[int(b), round(float(me[b]), 2), round(float(E[:, b].std()), 2)] for b in np.argsort(-me)[:12]]
 out["price_last_wg_counts"] = {int(k): int(v) for k, v in zip(*np.unique(E.argmax(1), return_counts=True))}
-out["config"] = {"m": a.m, "n": a.n, "eager": a.eager, "samples": a.samples,
+out["config"] = {"m": a.m, "n": a.n, "eager": a.eager, "samples": a.samples, "pricing": a.pricing,
                  "defer_tail": os.environ.get("SPX_DEFER_TAIL", "1") != "0"}
 print(json.dumps(out, indent=1))
