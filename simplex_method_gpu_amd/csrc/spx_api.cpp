@@ -315,6 +315,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
     SPX_TRY(x->alloc(&P.st, 1));
     SPX_TRY(x->alloc(&P.arrive, (size_t)(ARR_GROUPS * ARR_LINES * ARR_STRIDE)));
+    SPX_TRY(x->alloc(&P.tickets, (size_t)64));
+    P.price_dyn = env_off("SPX_PRICE_DYN") ? 0 : 1;
     if (x->opts.trace_cap < 0) return fail(SPX_ERR_ARG, "trace_cap must be >= 0");
     if (x->opts.trace_cap > 0) {
         P.trace_cap = x->opts.trace_cap;
@@ -572,12 +574,22 @@ int tab_rebuild(spx_ctx* x, bool slack) {
     return SPX_OK;
 }
 
+// k_price's column tickets (WM 2): each pass zeroes the other parity's
+// counter for the pass after it, so a pass that prices twice at one iteration
+// count (spx_price repeated, a basis set or rebuilt after the last pricing)
+// needs both cleared first
+int clear_tickets(spx_ctx* x) {
+    HIP_TRY(hipMemsetAsync(x->P.tickets, 0, 64 * sizeof(uint32_t), x->stream));
+    return SPX_OK;
+}
+
 int do_reset(spx_ctx* x) {
     const size_t mb = (size_t)(std::max<int64_t>(x->P.mloc, 1) * x->L) * sizeof(double);
     HIP_TRY(hipMemsetAsync(x->P.B0, 0, mb, x->stream));
     if (x->P.B1 != x->P.B0) HIP_TRY(hipMemsetAsync(x->P.B1, 0, mb, x->stream));
     for (double* v : {x->P.alpha0, x->P.alpha1, x->P.y0, x->P.y1, x->P.x_b, x->P.c_B})
         HIP_TRY(hipMemsetAsync(v, 0, (size_t)x->L * sizeof(double), x->stream));
+    SPX_TRY(clear_tickets(x));
     HIP_TRY(launch_reset(x->P, x->stream));
     HIP_TRY(launch_se_init(x->P, x->stream));  // steepest edge: gamma_j = 1 + ||A_j||^2
     if (x->P.bc) {  // B_w = I: no column list
@@ -940,6 +952,7 @@ int rv_prepare(spx_ctx* x) {
 int reinvert_basis(spx_ctx* x, const int64_t* basis) {
     if (x->P.row_shard) return fail(SPX_ERR_STATE, "basis reinversion needs replicated B^-1 (no row sharding)");
     SPX_TRY(rv_prepare(x));
+    SPX_TRY(clear_tickets(x));
     RvParams& R = x->rv;
     const int64_t m = x->m, ns = x->ns, L = x->L;
     std::vector<int32_t> owner((size_t)m, -1);
@@ -1610,6 +1623,7 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     ++x->n_eager;
     x->n_folds += fold ? 1 : 0;
     HIP_TRY(launch_se_prep(x->P, x->stream));
+    SPX_TRY(clear_tickets(x));
     HIP_TRY(launch_price(x->P, x->pcfg, x->stream, nullptr, nullptr));
     const int ps = x->P.pr_stride;
     if (x->use_comm) {

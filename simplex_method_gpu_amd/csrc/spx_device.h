@@ -233,6 +233,11 @@ struct Params {
     // in s_memrealtime ticks (100 MHz) in the first 32 words, then per-pass
     // clocks double-buffered by the pass parity (STAMP_*); nullptr in normal runs
     unsigned long long* stamps;
+    // k_price's dynamic tail (SPX_PRICE_DYN): a column-ticket counter per pass
+    // parity, each on its own 128-byte line (uint32 [2][32])
+    uint32_t* tickets;
+    int32_t price_dyn;  // 1: WM 2 pricing hands out its last columns by ticket (SPX_PRICE_DYN=0: off)
+    int32_t pad_dyn;
     // eta window (see above); win = KW, 0 = explicit B^-1 updated every pivot
     int32_t win;
     int32_t pad_w;

@@ -53,6 +53,9 @@ namespace spx {
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
+#ifndef SPX_PRICE_DYN_PCT
+#define SPX_PRICE_DYN_PCT 85  // the share of the columns handed out statically (grid stride)
+#endif
 #ifndef SPX_PRICE_PIPE
 #define SPX_PRICE_PIPE 1  // eta-window pricing: two 8-chunk batches of a column in flight
 #endif
@@ -539,6 +542,24 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const unsigned long long t_pw2 = P.stamps ? rtime() : 0ull;  // the staging is in LDS
     const int nlist = nb;
     const int stride = gridDim.x * WAVES;
+    // Dynamic tail (WM 2, C5: columns of 128 KB, 24 per wave, and a 60 us
+    // spread of workgroup ends; P.price_dyn): the first SPX_PRICE_DYN_PCT % of the
+    // list in grid-stride rounds as before, the rest one column per ticket,
+    // taken from a per-pass counter when a wave has finished its column (no
+    // older load is outstanding then, so nothing waits behind the atomic but
+    // the ticket itself).  Every column's terms and the argmin's total order
+    // are unchanged, so the same bits.  Workgroup 0 zeroes the next pass's
+    // counter (the other parity).  (With the base row in LDS, WM 1 at C3 /
+    // C4, the same tickets cost 30 and 125 us per pass: not used there.)
+    constexpr bool DYN = WM == 2;
+    int s_lim = nlist;
+    uint32_t* tkc = nullptr;
+    if (DYN && P.price_dyn) {
+        s_lim = stride * (int)(((int64_t)nlist * SPX_PRICE_DYN_PCT / 100) / stride);
+        if (s_lim < stride) s_lim = stride;
+        tkc = P.tickets + (it & 1) * 32;
+        if (wg0 && tid == 0) P.tickets[((it + 1) & 1) * 32] = 0u;
+    }
     // candidate update shared by every mode: Devex key, then the argmin
     auto consider = [&](int64_t j, double e, double wn, double dd) {
         double key = e;
@@ -613,7 +634,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // products without its stream (see below)
     auto unit_col = [&](int64_t jj) { return P.slack_unit && jj >= P.ns; };
     bool have = pre && !unit_col(j0);
-    for (int idx = idx0; idx < nlist; idx += stride) {
+    int idx_next = 0;
+    for (int idx = idx0; idx < nlist; idx = idx_next) {
         const bool first = idx == idx0;
         const int64_t j = first ? j0 : nbl(idx);
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
@@ -797,7 +819,15 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         }
         // next column's first chunks in flight during this column's reduction
-        const int nidx = idx + stride;
+        int nidx = idx + stride;
+        if constexpr (DYN) {
+            if (tkc && nidx >= s_lim) {  // (wave-uniform) the next column comes by ticket
+                uint32_t t = 0;
+                if (lane == 0) t = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nidx = s_lim + (int)__builtin_amdgcn_readfirstlane(t);
+            }
+        }
+        idx_next = nidx;
         const int64_t jn = nidx < nlist ? nbl(nidx) : 0;
         have = nidx < nlist && L2 >= CH * 64 && !unit_col(jn);
         if (have) {

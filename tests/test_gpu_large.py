@@ -100,3 +100,36 @@ def test_c5_invariants(spx, oracle):
 def test_global_y_large_m(spx, oracle):
     """m=20000: y no longer fits LDS, pricing reads it from global memory."""
     _check_invariants(spx, oracle, 20000, 21000, 1, 12, ncols=8)
+
+
+def test_dynamic_pricing_tail_same_bits(spx, monkeypatch):
+    """Eta-window pricing with the base row read from L2 (k_price WM 2, m large
+    enough that y_w and the base row do not both fit LDS: the C5 shape) hands
+    out its last columns by ticket in whatever order the waves finish
+    (Params::price_dyn).  Every column's terms and the argmin's total order do
+    not depend on which wave prices it, so the trace, the state and B^-1 are
+    those of the static grid stride (SPX_PRICE_DYN=0) bit for bit, through two
+    folds.  Then the stepped API prices twice at one iteration count (the
+    ticket counter of that pass parity must start from zero again) and
+    pivots."""
+    m, n, seed, k = 10000, 20000, 3, 130
+    outs = []
+    for dyn in ("1", "0"):
+        monkeypatch.setenv("SPX_PRICE_DYN", dyn)
+        with spx.Context(m=m, n=n, seed=seed, trace=k) as ctx:
+            cfg = ctx.config()
+            assert cfg["window"] == 64 and cfg["price_lds"] == 1  # y_w in LDS, the base row from L2
+            st, piv = ctx.iterate(k)
+            tp, tq = ctx.trace()
+            s = ctx.state()
+            p1, p2 = ctx.price(), ctx.price()
+            assert p1 == p2
+            q = ctx.pivot()
+            outs.append((piv, tp, tq, s, ctx.objective(), p1, q))
+    (pa, tpa, tqa, sa, za, p1a, qa), (pb, tpb, tqb, sb, zb, p1b, qb) = outs
+    assert pa == pb == k
+    assert p1a == p1b and qa == qb
+    assert np.array_equal(tpa, tpb) and np.array_equal(tqa, tqb)
+    for key in ("b_ixs", "x_b", "y"):
+        assert np.array_equal(sa[key], sb[key]), key
+    assert za == zb
