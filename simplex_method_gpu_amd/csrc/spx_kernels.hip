@@ -165,6 +165,9 @@ __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, i
                                              bool* timed_out = nullptr);
 template <int BLOCK, bool PLAIN>
 __device__ __forceinline__ UpdPartial reduce_partial_block(const UpdPartial& w, UpdPartial* red);
+template <int BLOCK>
+__device__ __forceinline__ UpdPartial reduce_partial_pair(const UpdPartial& wa, const UpdPartial& wb,
+                                                          UpdPartial* red);
 template <bool PLAIN = false>
 __device__ __forceinline__ UpdPartial upd_fetch(const Params& P, int g);
 __device__ __forceinline__ UpdPartial wave_reduce_partial(const UpdPartial& w);
