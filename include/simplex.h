@@ -111,8 +111,10 @@ typedef struct spx_opts {
  *          w_leave = max(w_p/alpha_q^2, 1); p = argmin of -e_j^2/w_j over
  *          e_j < -eps (first index on ties).  The pivot row comes free from
  *          the eta-window pricing pass (it computes r.A_j for every column),
- *          so DEVEX needs the window (opts.window 0 selects 64) and one rank.
- *          spx_price's min_e is then the entering column's reduced cost. */
+ *          so DEVEX needs the window (opts.window 0 selects 64).  On a column-
+ *          shard group the winner's record carries its reduced cost and weight
+ *          (not with SPX_FLAG_SPLIT_TAIL / SPX_RATIO_HARRIS).  spx_price's min_e
+ *          is then the entering column's reduced cost. */
 #define SPX_PRICING_DANTZIG 0
 #define SPX_PRICING_DEVEX   1
 /* STEEPEST: steepest edge with a recurrence (README.md:16-17): exact weights
@@ -124,8 +126,9 @@ typedef struct spx_opts {
  *          gamma_leave = max(gamma_p / alpha_q^2, 1); p = argmin of
  *          -e_j^2/gamma_j over e_j < -eps.  d_j rides on the pricing pass's
  *          A stream as a third dot (B_w^T alpha in LDS beside y_w and the base
- *          row, plus the window terms), so it needs the window and one rank,
- *          runs two-kernel passes, and not with the tableau.  spx_set_basis
+ *          row, plus the window terms), so it needs the window, runs two-kernel
+ *          passes, and not with the tableau; on a column-shard group as DEVEX
+ *          (every rank forms B_w^T alpha from the replicated B^-1).  spx_set_basis
  *          restarts the weights at 1 + ||A_j||^2. */
 #define SPX_PRICING_STEEPEST 2
 

@@ -342,7 +342,8 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.devex = (x->opts.pricing == SPX_PRICING_DEVEX || P.steep) ? 1 : 0;
     if (P.devex) {
         const char* rule = P.steep ? "steepest-edge" : "Devex";
-        if (G > 1) return fail(SPX_ERR_ARG, "%s pricing runs on one rank", rule);
+        if (G > 1 && P.split_tail) return fail(SPX_ERR_ARG, "%s pricing on a group needs the in-pass ratio-test tail (no split tail, no Harris)", rule);
+        if (G > 1 && (x->opts.flags & SPX_FLAG_ROW_SHARD)) return fail(SPX_ERR_ARG, "%s pricing needs replicated B^-1 (no row sharding)", rule);
         if (x->opts.window < 0) return fail(SPX_ERR_ARG, "%s pricing needs the eta window (window > 0 or 0 = auto)", rule);
         if (P.steep && (x->opts.flags & SPX_FLAG_TABLEAU)) return fail(SPX_ERR_ARG, "steepest-edge pricing runs without the tableau");
         if (x->opts.window == 0) KW = 64;
@@ -382,7 +383,10 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         SPX_TRY(x->alloc(&P.tab_list, (size_t)n));
         SPX_TRY(x->alloc(&P.tab_cnt, (size_t)1));
     }
-    P.pr_stride = P.win ? 1 + P.win / 2 : 1;
+    // the candidate record: {key, column}, then (eta window) the winner's KW
+    // window coefficients, then (Devex / steepest edge) its reduced cost and
+    // weight (dvx_payload)
+    P.pr_stride = P.win ? 1 + P.win / 2 + (P.devex ? 1 : 0) : 1;
 
     // column shard: structural and slack columns each split in G contiguous blocks
     int64_t rng[4];
@@ -1399,6 +1403,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 if (fold && x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));
                 if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
                 advance_window(x, fold);
+                HIP_TRY(launch_se_prep(x->P, x->stream));  // steepest edge: after the fold, before pricing
                 ++x->n_eager;
                 x->n_folds += fold ? 1 : 0;
                 Params Pp = x->P;  // the deferred ratio-test tail (each rank's own FTRAN partials)
@@ -1638,13 +1643,20 @@ int spx_price(spx_ctx* x, int64_t* p, double* min_e, int32_t* optimal) {
     HIP_TRY(hipStreamSynchronize(x->stream));
     HIP_TRY(hipMemcpy(cand.data(), x->P.price_in, sizeof(ArgMinEntry) * cand.size(), hipMemcpyDeviceToHost));
     ArgMinEntry best{INFINITY, INT64_MAX};
+    int gbest = 0;
     for (int g = 0; g < x->opts.nranks; ++g) {
         const ArgMinEntry& e = cand[(size_t)g * ps];
-        if (argmin_better(e.val, e.idx, best.val, best.idx)) best = e;
+        if (argmin_better(e.val, e.idx, best.val, best.idx)) {
+            best = e;
+            gbest = g;
+        }
     }
     if (p) *p = (best.idx == INT64_MAX) ? -1 : best.idx;
     double e_enter = best.val;
-    if (x->P.devex) HIP_TRY(hipMemcpy(&e_enter, x->P.dvx_e, sizeof(double), hipMemcpyDeviceToHost));
+    if (x->P.devex && x->opts.nranks > 1)  // the winner's record (dvx_payload)
+        std::memcpy(&e_enter, &cand[(size_t)gbest * ps + 1 + x->P.win / 2], sizeof(double));
+    else if (x->P.devex)
+        HIP_TRY(hipMemcpy(&e_enter, x->P.dvx_e, sizeof(double), hipMemcpyDeviceToHost));
     if (min_e) *min_e = e_enter;
     if (optimal) *optimal = no_entering(x->P, best.val, best.idx) ? 1 : 0;
     x->stepped_price = true;

@@ -587,7 +587,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                         w = fmax(w, g * g * dvx_wp);
                     }
                 }
-                if (lane == 0) P.W[j] = w;
+                if (lane == 0) {
+                    // (a group's last pricing workgroup reads the winner's weight back)
+                    if (P.nin > 1) st_agent(&P.W[j], w);
+                    else P.W[j] = w;
+                }
             }
             key = (e < -P.eps) ? -(e * e) / w : INFINITY;
         }
@@ -958,6 +962,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if (tid == 0) {
             P.price_out[0] = ArgMinEntry{t.val, t.idx};
             if (WIN && P.devex) *P.dvx_e = t.pad;
+            if (WIN && P.devex && P.nin > 1) {  // the reduced cost and weight travel with the record
+                double* ex = reinterpret_cast<double*>(P.price_out + 1 + KW / 2);
+                ex[0] = t.pad;
+                ex[1] = t.idx == INT64_MAX ? 1.0 : ld_agent(&P.W[t.idx]);
+            }
         }
         if (WIN && P.nin > 1) {
             double* wo = reinterpret_cast<double*>(P.price_out + 1);
@@ -1010,6 +1019,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if (tid == 0) {
         P.price_out[0] = ArgMinEntry{t.val, t.idx};
         if (WIN && P.devex) *P.dvx_e = t.pad;
+        if (WIN && P.devex && P.nin > 1) {  // the reduced cost and weight travel with the record
+            double* ex = reinterpret_cast<double*>(P.price_out + 1 + KW / 2);
+            ex[0] = t.pad;
+            ex[1] = t.idx == INT64_MAX ? 1.0 : ld_agent(&P.W[t.idx]);
+        }
     }
     if (WIN && P.nin > 1) {
         // the winner's window coefficients Wt[p][0..nw) travel with it (the
@@ -1291,6 +1305,13 @@ struct TailPre {
 // partial loads, instead of as a dependent pair at kernel entry
 __device__ __forceinline__ void tail_last(const Params& P, TailPre* t) {
     if (t && t->valid && t->kp >= 0) t->last = P.nb_list[t->cnt - 1];
+}
+
+// Devex / steepest edge on a column-shard group: the winning rank's record
+// carries the entering column's reduced cost and weight after its window
+// coefficients (Params::pr_stride), since only that rank prices the column
+__device__ __forceinline__ const double* dvx_payload(const Params& P, int gw) {
+    return reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1 + P.win / 2);
 }
 
 __device__ __forceinline__ TailPre tail_prefetch(const Params& P, int32_t nw, int32_t cnt, int64_t p) {
@@ -1612,6 +1633,13 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         p = p0;
         gw = gw0;
     }
+    const bool dvx_grp = P.devex && P.nin > 1;
+    double wp_grp = 1.0;
+    if (dvx_grp) {
+        const double* ex = dvx_payload(P, gw);
+        e_enter = ex[0];
+        wp_grp = ex[1];
+    }
     if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) return;
     wg0_mark(P, 0, t_wg0);
     unsigned long long* const slot = P.stamps ? P.stamps + 4 : nullptr;
@@ -1620,7 +1648,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
-            st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
+            st->min_e = (P.devex && (P.defer_price || dvx_grp)) ? e_enter : min_e;
             st->status = ST_OPTIMAL;
         }
         return;
@@ -1702,10 +1730,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
         ucv[u] = (WIN && u < nvalid && lane < tau) ? P.U[(lr0 + u) * P.win + lane] : 0.0;
     TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (!RS && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
-    if (P.defer_price) {
+    if (P.defer_price || dvx_grp) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
     }
+    if (dvx_grp) tpre.wp = wp_grp;
     const int64_t base = lr0 * L2;
     unsigned long long* const win = slot ? P.stamps + 16 : nullptr;
     stamp_stream(win, true);
@@ -2223,6 +2252,13 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
             if (argmin_better(e.val, e.idx, min_e, p)) { min_e = e.val; p = e.idx; gw = g; }
         }
     }
+    const bool dvx_grp = P.devex && P.nin > 1;
+    double wp_grp = 1.0;
+    if (dvx_grp) {
+        const double* ex = dvx_payload(P, gw);
+        e_enter = ex[0];
+        wp_grp = ex[1];
+    }
     if (Sv.status != ST_RUNNING || Sv.iter >= Sv.limit) {
         if (DEFER && blockIdx.x == 0 && tid == 0) P.trec->fresh = 0;  // no pivot: nothing deferred
         return;
@@ -2241,7 +2277,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     if (no_entering(P, min_e, p)) {  // OptimumFound (v4:299-302)
         if (blockIdx.x == 0 && tid == 0) {
             st->p = p;
-            st->min_e = (P.devex && P.defer_price) ? e_enter : min_e;
+            st->min_e = (P.devex && (P.defer_price || dvx_grp)) ? e_enter : min_e;
             st->status = ST_OPTIMAL;
             if (DEFER) P.trec->fresh = 0;
         }
@@ -2273,12 +2309,13 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
             rkp = P.nb_pos[p];
             rlast = P.nb_list[Sv.nb_count - 1];
         }
-        if (P.devex) rwp = P.W[p];
+        if (P.devex) rwp = dvx_grp ? wp_grp : P.W[p];
     }
-    if (P.defer_price) {
+    if (P.defer_price || dvx_grp) {
         tpre.has_e = true;
         tpre.e_enter = e_enter;
     }
+    if (dvx_grp) tpre.wp = wp_grp;
     const int64_t it = Sv.iter;
     const int par = (int)(it & 1);
     double* a_new = par ? P.alpha0 : P.alpha1;
@@ -2451,7 +2488,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
                 TailRec* rec = P.trec;
                 rec->it = it;
                 rec->p = p;
-                rec->e_rep = !P.devex ? min_e : (P.defer_price ? e_enter : *P.dvx_e);
+                rec->e_rep = !P.devex ? min_e : ((P.defer_price || dvx_grp) ? e_enter : *P.dvx_e);
                 rec->c_p = rc_p;
                 rec->wp = rwp;
                 rec->cnt = Sv.nb_count;
