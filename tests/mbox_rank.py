@@ -3,8 +3,9 @@ tests/test_gpu_mbox.py (not a test module).  The ranks exchange their
 mailbox handles through files in a directory, attach (spx_mbox_attach), run
 the pivots and store the state they reach.
 
-usage: python mbox_rank.py DIR RANK NRANKS M N SEED WINDOW K GRAPH_BATCH [SOLVE]
-(SOLVE 0: the state after K pivots only, no solve to the optimum)
+usage: python mbox_rank.py DIR RANK NRANKS M N SEED WINDOW K GRAPH_BATCH [SOLVE [PRICING]]
+(SOLVE 0: the state after K pivots only, no solve to the optimum; PRICING:
+spx_opts.pricing, 0 Dantzig by default)
 """
 import os
 import sys
@@ -20,7 +21,9 @@ import simplex_method_gpu_amd as spx  # noqa: E402
 def main():
     d, rank, G, m, n, seed, window, k, gb = sys.argv[1], *map(int, sys.argv[2:10])
     solve = int(sys.argv[10]) if len(sys.argv) > 10 else 1
-    with spx.Context(m=m, n=n, seed=seed, rank=rank, nranks=G, window=window, graph_batch=gb) as ctx:
+    pricing = int(sys.argv[11]) if len(sys.argv) > 11 else 0
+    with spx.Context(m=m, n=n, seed=seed, rank=rank, nranks=G, window=window, graph_batch=gb,
+                     pricing=pricing) as ctx:
         h = ctx.mbox_export()
         tmp = os.path.join(d, f"h{rank}.tmp")
         with open(tmp, "wb") as f:

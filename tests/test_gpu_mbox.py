@@ -122,3 +122,39 @@ def test_mbox_processes_deferred_tail(spx, tmp_path, graph_batch):
         for key in ("b_ixs", "x_b", "y", "binv"):
             assert np.array_equal(r[key], rs[key]), (g, key)
         assert float(r["z"]) == rz
+
+
+@pytest.mark.parametrize("pricing", [1, 2], ids=["devex", "steepest"])
+def test_mbox_processes_weighted_pricing(spx, tmp_path, pricing):
+    """Devex and steepest edge across two processes on one GPU (mailbox
+    exchange, captured passes): each record carries its winner's reduced cost
+    and weight; every rank reaches the single-rank state after K pivots and
+    the single rank's optimum, bit for bit."""
+    m, n, seed, k, G = 300, 1200, 8, 90, 2
+    with spx.Context(m=m, n=n, seed=seed, window=64, pricing=pricing) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+        rr = ref.solve()
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mbox_rank.py"), str(tmp_path), str(g), str(G),
+                               str(m), str(n), str(seed), "64", str(k), "16", "1", str(pricing)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=dict(os.environ)) for g in range(G)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for g, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {g}:\n{outs[g][-3000:]}"
+    assert rr.status == spx.SolveStatus.OptimumFound
+    for g in range(G):
+        r = np.load(tmp_path / f"r{g}.npz")
+        assert int(r["piv"]) == k
+        for key in ("b_ixs", "x_b", "y", "binv"):
+            assert np.array_equal(r[key], rs[key]), (g, key)
+        assert int(r["status"]) == int(spx.SolveStatus.OptimumFound)
+        assert int(r["pivots"]) == rr.pivots
+        assert float(r["z"]) == rr.z
