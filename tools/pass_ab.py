@@ -7,7 +7,8 @@ graph launch still runs 63 passes).
     SPX_DEFER_TAIL=0 python tools/pass_ab.py default   # env knobs apply to every build
     python tools/pass_ab.py env:SPX_FTRAN_RPW=1 env:SPX_FTRAN_RPW=4   # knobs per entry
     PASS_AB_M=1024 PASS_AB_N=4096 python tools/pass_ab.py ...          # another LP size
-    PASS_AB_PRICING=2 python tools/pass_ab.py ...                      # steepest edge"""
+    PASS_AB_PRICING=2 python tools/pass_ab.py ...                      # steepest edge
+    PASS_AB_WINDOW=64 python tools/pass_ab.py ...                      # Context(window=...)"""
 import json
 import os
 import subprocess
@@ -20,7 +21,7 @@ sys.path.insert(0, %r)
 import simplex_method_gpu_amd as spx
 best = 1e9
 with spx.Context(m=int(os.environ.get('PASS_AB_M', 4096)), n=int(os.environ.get('PASS_AB_N', 16384)), seed=0, device=0,
-                 pricing=int(os.environ.get('PASS_AB_PRICING', 0))) as ctx:
+                 pricing=int(os.environ.get('PASS_AB_PRICING', 0)), window=int(os.environ.get('PASS_AB_WINDOW', 0))) as ctx:
     ctx.iterate(63)
     for r in range(6):
         t0 = time.perf_counter()
