@@ -315,7 +315,7 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     SPX_TRY(x->alloc(&P.nb_pos, (size_t)n));
     SPX_TRY(x->alloc(&P.st, 1));
     SPX_TRY(x->alloc(&P.arrive, (size_t)(ARR_GROUPS * ARR_LINES * ARR_STRIDE)));
-    SPX_TRY(x->alloc(&P.tickets, (size_t)64));
+    SPX_TRY(x->alloc(&P.tickets, (size_t)TICKET_WORDS));
     P.price_dyn = env_off("SPX_PRICE_DYN") ? 0 : 1;
     if (x->opts.trace_cap < 0) return fail(SPX_ERR_ARG, "trace_cap must be >= 0");
     if (x->opts.trace_cap > 0) {
@@ -434,6 +434,18 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // keeps 4 columns in flight (k_price WM 3), so one pass over the list
     if (P.tab) pc.grid = (int)std::max<int64_t>(1, std::min(cap, (x->max_local_cols + 4 * waves - 1) / (4 * waves)));
     if (x->opts.price_grid > 0) pc.grid = x->opts.price_grid;
+    // the ticketed pricing tail (k_price, Params::price_dyn): with the base row
+    // read from L2 (WM 2, C5) always; with it in LDS (WM 1) only where a wave
+    // prices many columns (C4: 62; C3: 6, where the tickets cost more than the
+    // spread they remove)
+    if (pc.wm == 1 && x->max_local_cols < (int64_t)DYN1_MIN_COLS * pc.grid * (pc.block / 64)) P.price_dyn = 0;
+    // counters: measured (tools/pass_ab.py, 2 / 4 / 8 / 16) C4 664.6 / 627.9 / 635.2 / 633.8 us
+    // per pass, C5 1,032.3 / 1,023.9 / 1,022.0 / 1,010.7
+    P.tk_shards = pc.wm == 1 ? 4 : 16;
+    if (const char* e = std::getenv("SPX_TK_SHARDS")) {  // A/B
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 16) P.tk_shards = v;
+    }
 
     UpdateCfg& uc = x->ucfg;
     int ub = x->opts.update_block;
@@ -583,7 +595,7 @@ int tab_rebuild(spx_ctx* x, bool slack) {
 // count (spx_price repeated, a basis set or rebuilt after the last pricing)
 // needs both cleared first
 int clear_tickets(spx_ctx* x) {
-    HIP_TRY(hipMemsetAsync(x->P.tickets, 0, 64 * sizeof(uint32_t), x->stream));
+    HIP_TRY(hipMemsetAsync(x->P.tickets, 0, TICKET_WORDS * sizeof(uint32_t), x->stream));
     return SPX_OK;
 }
 

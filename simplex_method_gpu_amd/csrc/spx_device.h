@@ -112,6 +112,8 @@ struct alignas(16) RsHeader {
 constexpr int ARR_SHARDS = 8;
 constexpr int ARR_STRIDE = 32;  // uint32 per 128-byte line
 constexpr int ARR_LINES = 1 + ARR_SHARDS;
+constexpr int TICKET_WORDS = 2 * 16 * 32;  // k_price's ticket counters (Params::tk_shards <= 16)
+constexpr int DYN1_MIN_COLS = 16;          // WM 1 takes the ticketed tail from this many columns per wave
 enum : int { ARR_PRICE = 0, ARR_UPDATE = 1, ARR_FOLD = 2, ARR_GROUPS = 3 };
 // tagged ratio-test partial: 7 eight-byte fields as 14 {32-bit half, tag} words
 constexpr int UPD_WORDS = 14;
@@ -233,11 +235,11 @@ struct Params {
     // in s_memrealtime ticks (100 MHz) in the first 32 words, then per-pass
     // clocks double-buffered by the pass parity (STAMP_*); nullptr in normal runs
     unsigned long long* stamps;
-    // k_price's dynamic tail (SPX_PRICE_DYN): a column-ticket counter per pass
-    // parity, each on its own 128-byte line (uint32 [2][32])
+    // k_price's dynamic tail (SPX_PRICE_DYN): column-ticket counters, 16 per
+    // pass parity, each on its own 128-byte line (uint32 [2][16][32])
     uint32_t* tickets;
-    int32_t price_dyn;  // 1: WM 2 pricing hands out its last columns by ticket (SPX_PRICE_DYN=0: off)
-    int32_t pad_dyn;
+    int32_t price_dyn;  // 1: k_price hands out its last columns by ticket (SPX_PRICE_DYN=0: off)
+    int32_t tk_shards;  // ticket counters per pass parity (1..16)
     // eta window (see above); win = KW, 0 = explicit B^-1 updated every pivot
     int32_t win;
     int32_t pad_w;

@@ -53,6 +53,9 @@ namespace spx {
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
+#ifndef SPX_PRICE_DYN1
+#define SPX_PRICE_DYN1 1  // k_price WM 1 (base row in LDS): the ticketed tail where the host enables it (C4)
+#endif
 #ifndef SPX_PRICE_DYN_PCT
 #define SPX_PRICE_DYN_PCT 85  // the share of the columns handed out statically (grid stride)
 #endif
@@ -545,24 +548,32 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const unsigned long long t_pw2 = P.stamps ? rtime() : 0ull;  // the staging is in LDS
     const int nlist = nb;
     const int stride = gridDim.x * WAVES;
-    // Dynamic tail (WM 2, C5: columns of 128 KB, 24 per wave, and a 60 us
-    // spread of workgroup ends; P.price_dyn): the first SPX_PRICE_DYN_PCT % of the
-    // list in grid-stride rounds as before, the rest one column per ticket,
-    // taken from a per-pass counter when a wave has finished its column (no
-    // older load is outstanding then, so nothing waits behind the atomic but
-    // the ticket itself).  Every column's terms and the argmin's total order
-    // are unchanged, so the same bits.  Workgroup 0 zeroes the next pass's
-    // counter (the other parity).  (With the base row in LDS, WM 1 at C3 /
-    // C4, the same tickets cost 30 and 125 us per pass: not used there.)
-    constexpr bool DYN = WM == 2;
+    // Dynamic tail (P.price_dyn: WM 2, C5, and WM 1 where a wave prices many
+    // columns, C4): the first SPX_PRICE_DYN_PCT % of the list in grid-stride
+    // rounds as before, the rest one column per ticket.  P.tk_shards
+    // counters (a 128-byte line each, per pass parity): counter k hands out
+    // the slots s_lim + k + SHARDS t, and a wave draws from the counter its
+    // (workgroup / 8, wave) pair selects, so every counter serves waves of all
+    // eight XCDs (blockIdx % 8) and no address takes more than 1/SHARDS of the
+    // fetch-adds (one address: same-address atomics run one after another in
+    // their L2 channel, ~8 ns each).  A wave takes each ticket one column
+    // ahead -- the first as it starts its last static column, the next as it
+    // starts a ticketed one -- so the round trip overlaps a column's stream.
+    // Every column's terms and the argmin's total order are unchanged, so the
+    // same bits.  Workgroup 0 zeroes the next pass's counters (the other
+    // parity).
+    constexpr bool DYN = WM == 2 || (SPX_PRICE_DYN1 && WM == 1);
+    const int TKS = P.tk_shards;  // (1..16, the host's choice per pricing mode)
     int s_lim = nlist;
     uint32_t* tkc = nullptr;
+    const int tk_k = (int)((blockIdx.x / 8 + 2 * wave) % TKS);
     if (DYN && P.price_dyn) {
         s_lim = stride * (int)(((int64_t)nlist * SPX_PRICE_DYN_PCT / 100) / stride);
         if (s_lim < stride) s_lim = stride;
-        tkc = P.tickets + (it & 1) * 32;
-        if (wg0 && tid == 0) P.tickets[((it + 1) & 1) * 32] = 0u;
+        if (s_lim < nlist) tkc = P.tickets + ((it & 1) * TKS + tk_k) * 32;
+        if (wg0 && tid < TKS) P.tickets[(((it + 1) & 1) * TKS + tid) * 32] = 0u;
     }
+    uint32_t tk_pend = 0;  // the ticket taken ahead (lane 0)
     // candidate update shared by every mode: Devex key, then the argmin
     auto consider = [&](int64_t j, double e, double wn, double dd) {
         double key = e;
@@ -644,6 +655,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     int idx_next = 0;
     for (int idx = idx0; idx < nlist; idx = idx_next) {
         const bool first = idx == idx0;
+        if constexpr (DYN) {
+            if (tkc && idx < s_lim && idx + stride >= s_lim) {  // the last static column: the first ticket
+                uint32_t t = 0;
+                if (lane == 0) t = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tk_pend = t;
+            }
+        }
         const int64_t j = first ? j0 : nbl(idx);
         const dbl2* __restrict__ col = reinterpret_cast<const dbl2*>(P.A + j * L);
         double wv = 0.0;
@@ -828,10 +846,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         // next column's first chunks in flight during this column's reduction
         int nidx = idx + stride;
         if constexpr (DYN) {
-            if (tkc && nidx >= s_lim) {  // (wave-uniform) the next column comes by ticket
-                uint32_t t = 0;
-                if (lane == 0) t = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                nidx = s_lim + (int)__builtin_amdgcn_readfirstlane(t);
+            if (tkc && nidx >= s_lim) {  // (wave-uniform) the next column comes by the ticket taken ahead
+                nidx = s_lim + tk_k + TKS * (int)__builtin_amdgcn_readfirstlane(tk_pend);
+                if (nidx < nlist) {
+                    uint32_t t = 0;
+                    if (lane == 0) t = __hip_atomic_fetch_add(tkc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    tk_pend = t;
+                }
             }
         }
         idx_next = nidx;

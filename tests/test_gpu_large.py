@@ -133,3 +133,26 @@ def test_dynamic_pricing_tail_same_bits(spx, monkeypatch):
     for key in ("b_ixs", "x_b", "y"):
         assert np.array_equal(sa[key], sb[key]), key
     assert za == zb
+
+
+def test_dynamic_pricing_tail_wm1_same_bits(spx, monkeypatch):
+    """The ticketed tail with the base row in LDS (k_price WM 1), where a wave
+    prices at least 16 columns (the C4 shape; m=2048, n=40960: 19 per wave):
+    the same trace, state and objective bits as the static grid stride
+    (SPX_PRICE_DYN=0), through two folds."""
+    m, n, seed, k = 2048, 40960, 4, 130
+    outs = []
+    for dyn in ("1", "0"):
+        monkeypatch.setenv("SPX_PRICE_DYN", dyn)
+        with spx.Context(m=m, n=n, seed=seed, trace=k) as ctx:
+            cfg = ctx.config()
+            assert cfg["window"] == 64 and cfg["price_lds"] == 2  # y_w and the base row in LDS
+            st, piv = ctx.iterate(k)
+            tp, tq = ctx.trace()
+            outs.append((piv, tp, tq, ctx.state(), ctx.objective()))
+    (pa, tpa, tqa, sa, za), (pb, tpb, tqb, sb, zb) = outs
+    assert pa == pb == k
+    assert np.array_equal(tpa, tpb) and np.array_equal(tqa, tqb)
+    for key in ("b_ixs", "x_b", "y"):
+        assert np.array_equal(sa[key], sb[key]), key
+    assert za == zb
