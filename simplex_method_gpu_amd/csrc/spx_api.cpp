@@ -438,7 +438,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // read from L2 (WM 2, C5) always; with it in LDS (WM 1) only where a wave
     // prices many columns (C4: 62; C3: 6, where the tickets cost more than the
     // spread they remove)
-    if (pc.wm == 1 && x->max_local_cols < (int64_t)DYN1_MIN_COLS * pc.grid * (pc.block / 64)) P.price_dyn = 0;
+    if (pc.wm == 1 && x->max_local_cols < (int64_t)DYN1_MIN_COLS * pc.grid * (pc.block / 64) &&
+        !(std::getenv("SPX_PRICE_DYN") && std::getenv("SPX_PRICE_DYN")[0] == '2'))  // (2: A/B, on regardless)
+        P.price_dyn = 0;
     // counters: measured (tools/pass_ab.py, 2 / 4 / 8 / 16) C4 664.6 / 627.9 / 635.2 / 633.8 us
     // per pass, C5 1,032.3 / 1,023.9 / 1,022.0 / 1,010.7
     P.tk_shards = pc.wm == 1 ? 4 : 16;
