@@ -448,6 +448,9 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         const int v = std::atoi(e);
         if (v >= 1 && v <= 16) P.tk_shards = v;
     }
+    // every counter must have waves drawing from it (k_price: counter
+    // (wave + workgroup) mod shards reaches WAVES + grid - 1 counters)
+    P.tk_shards = (int32_t)std::min<int64_t>(P.tk_shards, (int64_t)pc.block / 64 + pc.grid - 1);
 
     UpdateCfg& uc = x->ucfg;
     int ub = x->opts.update_block;

@@ -552,9 +552,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // columns, C4): the first SPX_PRICE_DYN_PCT % of the list in grid-stride
     // rounds as before, the rest one column per ticket.  P.tk_shards
     // counters (a 128-byte line each, per pass parity): counter k hands out
-    // the slots s_lim + k + SHARDS t, and a wave draws from the counter its
-    // (workgroup / 8, wave) pair selects, so every counter serves waves of all
-    // eight XCDs (blockIdx % 8) and no address takes more than 1/SHARDS of the
+    // the slots s_lim + k + SHARDS t, and a wave draws from counter
+    // (wave + workgroup) mod SHARDS: workgroups b .. b + 7 all reach counter
+    // b + 7, so every counter serves waves of all eight XCDs (blockIdx % 8),
+    // and every counter has waves when WAVES + grid - 1 >= SHARDS (the host
+    // caps the count so; a counter nobody draws from would leave its slots
+    // unpriced).  No address takes more than 1/SHARDS of the
     // fetch-adds (one address: same-address atomics run one after another in
     // their L2 channel, ~8 ns each).  A wave takes each ticket one column
     // ahead -- the first as it starts its last static column, the next as it
@@ -566,7 +569,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     const int TKS = P.tk_shards;  // (1..16, the host's choice per pricing mode)
     int s_lim = nlist;
     uint32_t* tkc = nullptr;
-    const int tk_k = (int)((blockIdx.x / 8 + 2 * wave) % TKS);
+    const int tk_k = (int)((wave + blockIdx.x) % TKS);
     if (DYN && P.price_dyn) {
         s_lim = stride * (int)(((int64_t)nlist * SPX_PRICE_DYN_PCT / 100) / stride);
         if (s_lim < stride) s_lim = stride;

@@ -156,3 +156,23 @@ def test_dynamic_pricing_tail_wm1_same_bits(spx, monkeypatch):
     for key in ("b_ixs", "x_b", "y"):
         assert np.array_equal(sa[key], sb[key]), key
     assert za == zb
+
+
+@pytest.mark.parametrize("grid", [1, 2, 3])
+def test_dynamic_pricing_tail_small_grids(spx, monkeypatch, grid):
+    """The ticketed tail with 1-3 pricing workgroups (8-24 waves; the
+    counters capped to the waves that draw from them, none left without
+    one): the static order's bits (m=300, n=1200, window 16, 130 pivots)."""
+    m, n, seed, k = 300, 1200, 7, 130
+    outs = []
+    for dyn in ("2", "0"):
+        monkeypatch.setenv("SPX_PRICE_DYN", dyn)
+        with spx.Context(m=m, n=n, seed=seed, window=16, persist=False, price_grid=grid, trace=k) as ctx:
+            st, piv = ctx.iterate(k)
+            tp, tq = ctx.trace()
+            outs.append((piv, tp, tq, ctx.state()))
+    (pa, tpa, tqa, sa), (pb, tpb, tqb, sb) = outs
+    assert pa == pb == k
+    assert np.array_equal(tpa, tpb) and np.array_equal(tqa, tqb)
+    for key in ("b_ixs", "x_b", "y"):
+        assert np.array_equal(sa[key], sb[key]), key
