@@ -451,6 +451,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     // every counter must have waves drawing from it (k_price: counter
     // (wave + workgroup) mod shards reaches WAVES + grid - 1 counters)
     P.tk_shards = (int32_t)std::min<int64_t>(P.tk_shards, (int64_t)pc.block / 64 + pc.grid - 1);
+    pc.tk = pc.wm == 1 && P.price_dyn;
+    if (pc.tk) {  // (its own instantiation: the LDS attribute set for it too)
+        int per_cu_tk = 0;
+        HIP_TRY(price_prepare(pc, &per_cu_tk));
+    }
 
     UpdateCfg& uc = x->ucfg;
     int ub = x->opts.update_block;

@@ -13,6 +13,7 @@ struct PriceCfg {
                        // 4 / 5 = 1 / 2 with steepest edge (B_w^T alpha in LDS / global)
     size_t lds_bytes;  // dynamic LDS per workgroup
     int grid;          // workgroups (persistent-style, grid-stride over columns)
+    bool tk = false;   // wm 1: the instantiation with the ticketed tail (Params::price_dyn)
 };
 
 struct UpdateCfg {

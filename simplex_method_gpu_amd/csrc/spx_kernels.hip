@@ -53,9 +53,6 @@ namespace spx {
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
-#ifndef SPX_PRICE_DYN1
-#define SPX_PRICE_DYN1 1  // k_price WM 1 (base row in LDS): the ticketed tail where the host enables it (C4)
-#endif
 #ifndef SPX_PRICE_DYN_PCT
 #define SPX_PRICE_DYN_PCT 85  // the share of the columns handed out statically (grid stride)
 #endif
@@ -177,7 +174,10 @@ __device__ __forceinline__ UpdPartial wave_reduce_partial(const UpdPartial& w);
 // the deferred ratio-test tail's bookkeeping (TailRec; defined with the tail)
 __device__ __forceinline__ void apply_deferred_tail(const Params& P, DevState* st, const TailRec& R,
                                                     const UpdPartial& t);
-template <int BLOCK, bool LDS_Y, int WM>
+// TK: the ticketed tail compiled in for WM 1 (a separate instantiation, so the
+// static C3 pass keeps its code: carrying the disabled ticket branches cost
+// it 0.5 us per pass); WM 2 always carries it
+template <int BLOCK, bool LDS_Y, int WM, bool TK = false>
 __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     DevState* st = P.st;
     constexpr int WAVES = BLOCK / 64;
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // Every column's terms and the argmin's total order are unchanged, so the
     // same bits.  Workgroup 0 zeroes the next pass's counters (the other
     // parity).
-    constexpr bool DYN = WM == 2 || (SPX_PRICE_DYN1 && WM == 1);
+    constexpr bool DYN = WM == 2 || (TK && WM == 1);
     const int TKS = P.tk_shards;  // (1..16, the host's choice per pricing mode)
     int s_lim = nlist;
     uint32_t* tkc = nullptr;
@@ -3093,26 +3093,26 @@ __global__ void k_reset(Params P) {
 // ---------------------------------------------------------------------------
 // Host-side launchers
 // ---------------------------------------------------------------------------
-template <int BLOCK, bool LDS_Y, int WM>
+template <int BLOCK, bool LDS_Y, int WM, bool TK = false>
 static hipError_t launch_price_t(const Params& P, int grid, size_t lds, hipStream_t s, hipEvent_t e0,
                                  hipEvent_t e1) {
     if (e0 || e1) {
-        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM, TK>), dim3(grid), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     } else {
-        hipLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM>), dim3(grid), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_price<BLOCK, LDS_Y, WM, TK>), dim3(grid), dim3(BLOCK), lds, s, P);
     }
     return hipGetLastError();
 }
 
-template <int BLOCK, bool LDS_Y, int WM>
+template <int BLOCK, bool LDS_Y, int WM, bool TK = false>
 static hipError_t prep_price_t(size_t lds, int* blocks_per_cu) {
     hipError_t e = hipSuccess;
     if (lds > 65536) {
-        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_price<BLOCK, LDS_Y, WM>),
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_price<BLOCK, LDS_Y, WM, TK>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_price<BLOCK, LDS_Y, WM>, BLOCK, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_price<BLOCK, LDS_Y, WM, TK>, BLOCK, lds);
 }
 
 // (lds_y, wm) variants: (1,0) (0,0) explicit B^-1; (1,1) (1,2) (0,2) eta window
@@ -3126,7 +3126,11 @@ static hipError_t price_dispatch(const PriceCfg& c, const Params* P, hipStream_t
         if (c.lds_y) SPX_PV(true, 0);
         SPX_PV(false, 0);
     }
-    if (c.wm == 1 && c.lds_y) SPX_PV(true, 1);
+    if (c.wm == 1 && c.lds_y) {
+        if (c.tk) return P ? launch_price_t<BLOCK, true, 1, true>(*P, c.grid, c.lds_bytes, s, e0, e1)
+                           : prep_price_t<BLOCK, true, 1, true>(c.lds_bytes, blocks_per_cu);
+        SPX_PV(true, 1);
+    }
     if (c.wm == 2) {
         if (c.lds_y) SPX_PV(true, 2);
         SPX_PV(false, 2);
