@@ -47,6 +47,82 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+class Watchdog:
+    """Multi-rank bench guard (one per rank): each phase of the run (a timed
+    window, the next windows, one spx_iterate call of the whole solve, ...)
+    is armed with a bound; if the phase has not ended by then -- a lost peer,
+    a hung all-gather or mailbox poll -- this rank prints its rank, the phase,
+    the host's pivot count and spx_dispatch_stats to stderr and exits with
+    status 3 from a watcher thread (os._exit: no re-exec, nothing else runs on
+    the GPU).  Off (seconds <= 0) on one rank unless asked for."""
+
+    EXIT = 3
+
+    def __init__(self, seconds, rank, out=None):
+        import threading
+
+        self.seconds = float(seconds)
+        self.rank = rank
+        self.out = out or sys.stderr
+        self._cv = threading.Condition()
+        self._phase = None
+        self._deadline = None
+        self._ctx = None
+        self._gen = 0
+        if self.seconds > 0:
+            threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def arm(self, phase, ctx=None, seconds=None):
+        with self._cv:
+            self._phase, self._ctx = phase, ctx
+            self._deadline = time.monotonic() + (self.seconds if seconds is None else float(seconds))
+            self._gen += 1
+            self._cv.notify()
+
+    def disarm(self):
+        with self._cv:
+            self._phase = self._deadline = self._ctx = None
+            self._gen += 1
+            self._cv.notify()
+
+    def phase(self, name, ctx=None, seconds=None):
+        wd = self
+
+        class _P:
+            def __enter__(self_):
+                wd.arm(name, ctx, seconds)
+                return wd
+
+            def __exit__(self_, *exc):
+                wd.disarm()
+        return _P()
+
+    def _report(self, phase, ctx):
+        msg = {"watchdog": "bound exceeded", "rank": self.rank, "phase": phase, "bound_s": self.seconds}
+        if ctx is not None:
+            try:
+                msg["dispatch_stats"] = ctx.dispatch_stats()
+                msg["pivots_at_last_readback"] = getattr(ctx, "last_pivots", None)
+            except Exception as e:  # the report must not hang or raise
+                msg["dispatch_stats"] = f"unavailable: {e}"
+        print("bench.py: " + json.dumps(msg), file=self.out, flush=True)
+
+    def _watch(self):
+        while True:
+            with self._cv:
+                while self._deadline is None:
+                    self._cv.wait()
+                gen, left = self._gen, self._deadline - time.monotonic()
+                if left > 0:
+                    self._cv.wait(left)
+                    continue
+                if gen != self._gen:
+                    continue
+                phase, ctx = self._phase, self._ctx
+            self._report(phase, ctx)
+            os._exit(self.EXIT)
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CONFIGS = {"C2": (1024, 4096), "C3": (4096, 16384), "C4": (4096, 131072), "C5": (16384, 65536)}
 METRIC = "simplex iterations/sec on dense m={m} n={n} fp64; achieved HBM GB/s"  # BASELINE.json at C3
@@ -93,6 +169,9 @@ def parse():
     ap.add_argument("--minloc", choices=["rccl", "mbox"], default="rccl",
                     help="N > 1: the pricing MINLOC exchange as an RCCL all-gather (default) or as direct "
                          "stores into the peers' mailboxes (spx_mbox_attach, one small kernel per pass)")
+    ap.add_argument("--watchdog", type=float, default=None,
+                    help="seconds a phase (a timed window, one iterate call of the whole solve, ...) may take "
+                         "before this rank reports where it is and exits 3 (default: 120 with N > 1, off on one rank)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of --gpus N on a one-GPU box: every rank on GPU 0 (gloo process group, "
                          "mailbox MINLOC; RCCL refuses two ranks on one device). Exercises the multi-rank "
@@ -140,6 +219,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import simplex_method_gpu_amd as spx
 
+    wd = Watchdog(args.watchdog if args.watchdog is not None else (120.0 if multi else 0.0), rank)
     m, n = args.m, args.n
     row_shard = multi and args.row_shard
 
@@ -189,7 +269,9 @@ def main():
         pivots between barriers and device syncs.  Returns the max-over-ranks
         time and what ran; with `spread`, also the max-over-ranks times of the
         next three windows, each timed on its own."""
-        ctx = make(events, window)
+        with wd.phase("context + warm-up" + (" (event-timed)" if events else "")):
+            ctx = make(events, window)
+        wd.arm("warm-up" + (" (event-timed)" if events else ""), ctx)
         cfg = ctx.config()
         kw = cfg["window"]
         # whole windows (eta window), or whole captured batches of passes
@@ -209,6 +291,7 @@ def main():
             ctx.pass_times()  # drop the warm-up's and the lead's events
             ctx.loop_times()
         d0 = ctx.dispatch_stats()
+        wd.arm("timed window" + (" (event-timed)" if events else ""), ctx)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -217,12 +300,17 @@ def main():
         barrier()
         dt = reduce_max([time.perf_counter() - t0])[0]
         d1 = ctx.dispatch_stats()
+        # the averages behind the roofline cover the timed region, not the
+        # windows timed after it
+        info1 = ctx.info()
+        cols = ctx.ftran_cols()
         delta = {k: d1[k] - d0[k] for k in ("eager_passes", "graph_launches", "graph_passes",
                                             "persistent_launches", "persistent_passes", "folds", "graph_builds")}
         windows = None
         if spread and st == 0:
             ts, pv = [], piv1
-            for _ in range(3):
+            for k in range(3):
+                wd.arm(f"next window {k + 1}", ctx)
                 barrier()
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
@@ -243,10 +331,10 @@ def main():
                 pt = {"passes": np_, "price_ms": 1e-3 * lt["price_us"],
                       "price_minloc_ms": 1e-3 * lt["price_us"], "update_ms": 1e-3 * lt["ftran_us"],
                       "loop_ms_per_pass": lt["loop_ms"] / max(lt["loop_passes"], 1)}
-        info1 = ctx.info()
-        cols = ctx.ftran_cols()
+        wd.arm("readback", ctx)
         comm = ctx.comm_info()
         ctx.close()
+        wd.disarm()
         return {"cfg": cfg, "dt": dt, "pivots": piv1 - piv0, "steps": steps, "lead": lead + warm, "dispatch": delta,
                 "windows_s_per_pivot": windows,
                 "pt": pt, "lt": lt, "nb": 0.5 * (info0["local_nonbasic"] + info1["local_nonbasic"]),
@@ -329,11 +417,12 @@ def main():
 
     sharded = None
     if not args.no_sharded_pricing and (m, n) != CONFIGS["C4"]:
-        sharded = sharded_pricing_block(make, reduce_max, reduce_sum, world, args)
+        with wd.phase("pricing_c4 (C4 sharded pricing window)"):
+            sharded = sharded_pricing_block(make, reduce_max, reduce_sum, world, args)
 
     to_opt = None
     if not args.no_solve_to_optimum:
-        to_opt = solve_to_optimum_block(make, barrier, reduce_max, torch, args.window, main_run, value)
+        to_opt = solve_to_optimum_block(make, barrier, reduce_max, torch, args.window, main_run, value, wd)
 
     steep = None
     if world == 1 and not multi and not args.no_steepest and win > 0:
@@ -479,7 +568,7 @@ def main():
         dist.destroy_process_group()
 
 
-def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, value):
+def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, value, wd):
     """The whole solve of the headline LP: the default path from the slack
     basis to optimality on the same clock as `value` (barrier + device sync on
     both sides, max over ranks), dispatched as the library does it (captured
@@ -487,15 +576,19 @@ def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, v
     spx_iterate call).  `value` samples an early window, where the compact
     FTRAN operand is narrow (S columns of B_w that are not unit); S grows over
     the solve, and so does the FTRAN pass."""
-    ctx = make(False, window)
+    with wd.phase("solve_to_optimum: context"):
+        ctx = make(False, window)
     try:
         cols0 = ctx.ftran_cols()
+        wd.arm("solve_to_optimum: start", ctx)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st, piv = ctx.iterate(0)
         while st == 0:  # SolveStatus.MaxIter: not terminated yet
+            wd.arm(f"solve_to_optimum: iterate(4096) from pivot {piv}", ctx)  # one call's bound
             st, piv = ctx.iterate(4096)
+        wd.arm("solve_to_optimum: end", ctx)
         torch.cuda.synchronize()
         barrier()
         dt = reduce_max([time.perf_counter() - t0])[0]
@@ -504,6 +597,7 @@ def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, v
         ds = ctx.dispatch_stats()
     finally:
         ctx.close()
+        wd.disarm()
     rate = piv / dt if dt > 0 else 0.0
     return {"status": ["MaxIter", "OptimumFound", "Unbounded", "ThetaOverflow"][int(st)], "pivots": int(piv),
             "seconds": dt, "iterations_per_s": rate, "z": z,

@@ -265,6 +265,7 @@ class Context:
     def iterate(self, k: int):
         st, piv = ctypes.c_int32(), ctypes.c_int64()
         check(self._L.spx_iterate(self._h, k, ctypes.byref(st), ctypes.byref(piv)))
+        self.last_pivots = piv.value  # (host-side: read by bench.py's watchdog without a device call)
         return SolveStatus(st.value), piv.value
 
     def solve(self, max_iter: int = (1 << 62)) -> SolveResult:

@@ -449,12 +449,23 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
         if (v >= 1 && v <= 16) P.tk_shards = v;
     }
     // every counter must have waves drawing from it (k_price: counter
-    // (wave + workgroup) mod shards reaches WAVES + grid - 1 counters)
-    P.tk_shards = (int32_t)std::min<int64_t>(P.tk_shards, (int64_t)pc.block / 64 + pc.grid - 1);
+    // (wave + workgroup) mod shards reaches WAVES + grid - 1 counters);
+    // SPX_TK_UNSAFE=1 skips the cap (tests: k_price's coverage check must
+    // then stop the solve)
+    if (!env_on("SPX_TK_UNSAFE"))
+        P.tk_shards = (int32_t)std::min<int64_t>(P.tk_shards, (int64_t)pc.block / 64 + pc.grid - 1);
     pc.tk = pc.wm == 1 && P.price_dyn;
     if (pc.tk) {  // (its own instantiation: the LDS attribute set for it too)
         int per_cu_tk = 0;
         HIP_TRY(price_prepare(pc, &per_cu_tk));
+        // the grid was sized from the static instantiation's occupancy: if the
+        // ticketed one holds fewer workgroups per CU, size it from that, so the
+        // grid stays one dispatch round (and re-cap the counters to it)
+        if (per_cu_tk >= 1 && per_cu_tk < per_cu && x->opts.price_grid <= 0) {
+            pc.grid = (int)std::max<int64_t>(1, std::min<int64_t>(pc.grid, (int64_t)x->cus * per_cu_tk));
+            if (!env_on("SPX_TK_UNSAFE"))
+                P.tk_shards = (int32_t)std::min<int64_t>(P.tk_shards, (int64_t)pc.block / 64 + pc.grid - 1);
+        }
     }
 
     UpdateCfg& uc = x->ucfg;
@@ -764,6 +775,24 @@ int build_graph(spx_ctx* x) {
     return SPX_OK;
 }
 
+// The ticketed pricing tail's coverage (k_price, Params::price_dyn): each
+// pass's workgroup 0 checks the previous pass's counters on the device
+// (DevState::uncovered); the last pass of a call is checked here, from its
+// counters and the slots each had to hand out (word 1 of its line).
+int check_tickets(spx_ctx* x) {
+    bool bad = x->st_host->uncovered != 0;
+    if (!bad && x->P.price_dyn && (x->pcfg.wm == 2 || x->pcfg.tk)) {
+        uint32_t t[TICKET_WORDS];
+        HIP_TRY(hipMemcpy(t, x->P.tickets, sizeof(t), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 2 * x->P.tk_shards; ++k) bad = bad || t[32 * k + 1] > t[32 * k];
+    }
+    if (bad) {
+        return fail(SPX_ERR_STATE, "pricing: ticketed list slots were left unpriced (tk_shards %d, grid %d): the "
+                    "entering column may be wrong; call spx_reset", x->P.tk_shards, x->pcfg.grid);
+    }
+    return SPX_OK;
+}
+
 int read_state(spx_ctx* x) {
     HIP_TRY(hipMemcpyAsync(x->st_host, x->P.st, sizeof(DevState), hipMemcpyDeviceToHost, x->stream));
     HIP_TRY(hipStreamSynchronize(x->stream));
@@ -772,6 +801,7 @@ int read_state(spx_ctx* x) {
     x->nw = x->st_host->nw;
     if (x->status == ST_WINDOW_FULL) return fail(SPX_ERR_STATE, "internal error: eta window overflow");
     if (x->status == ST_HANDOFF_TIMEOUT) return fail(SPX_ERR_STATE, "internal error: ratio-test hand-off timed out");
+    SPX_TRY(check_tickets(x));
     return SPX_OK;
 }
 
@@ -902,6 +932,10 @@ int iterate_persist(spx_ctx* x, int64_t k) {
         HIP_TRY(hipMemsetAsync(x->la.ls, 0, sizeof(LoopState), x->stream));
         x->persist = false;
         ++x->n_persist_fallback;
+        // k_loop never touches k_price's column tickets, and each two-kernel
+        // pass only zeroes the other parity's: a stepped spx_price before the
+        // persistent launches can have left this parity's counters used
+        SPX_TRY(clear_tickets(x));
         x->nw = x->P.win ? x->st_host->nw : 0;
         const int64_t left = target - x->pivots;
         if (x->status == SPX_STATUS_MAX_ITER && left > 0) return iterate_raw(x, left);

@@ -158,7 +158,7 @@ struct alignas(16) DevState {
     uint32_t pad_t0;     // (the arrival counters live in Params::arrive)
     uint32_t pad_t1;
     int32_t nw;          // eta window: pivots since the last fold (nw-1 pending)
-    uint32_t pad_t2;
+    uint32_t uncovered;  // set by k_price: a pass's ticketed list slots were not all taken (never cleared but by a reset)
     int32_t pad1;
     int64_t leave;       // Devex: column that left at the last pivot (-1 none)
     double wp;           // Devex: weight of the last entering column

@@ -557,14 +557,19 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // b + 7, so every counter serves waves of all eight XCDs (blockIdx % 8),
     // and every counter has waves when WAVES + grid - 1 >= SHARDS (the host
     // caps the count so; a counter nobody draws from would leave its slots
-    // unpriced).  No address takes more than 1/SHARDS of the
+    // unpriced, which the pass after this one checks on the device: every
+    // counter's last value must reach the slots it hands out, else
+    // DevState::uncovered is set and the host fails the call).  No address
+    // takes more than 1/SHARDS of the
     // fetch-adds (one address: same-address atomics run one after another in
     // their L2 channel, ~8 ns each).  A wave takes each ticket one column
     // ahead -- the first as it starts its last static column, the next as it
     // starts a ticketed one -- so the round trip overlaps a column's stream.
     // Every column's terms and the argmin's total order are unchanged, so the
-    // same bits.  Workgroup 0 zeroes the next pass's counters (the other
-    // parity).
+    // same bits.  Workgroup 0 writes how many tickets of each counter this
+    // pass needs (word 1 of its line); at its end it checks the previous
+    // pass's counters (the other parity) against theirs and zeroes them for
+    // the next pass.
     constexpr bool DYN = WM == 2 || (TK && WM == 1);
     const int TKS = P.tk_shards;  // (1..16, the host's choice per pricing mode)
     int s_lim = nlist;
@@ -573,8 +578,13 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     if (DYN && P.price_dyn) {
         s_lim = stride * (int)(((int64_t)nlist * SPX_PRICE_DYN_PCT / 100) / stride);
         if (s_lim < stride) s_lim = stride;
-        if (s_lim < nlist) tkc = P.tickets + ((it & 1) * TKS + tk_k) * 32;
-        if (wg0 && tid < TKS) P.tickets[(((it + 1) & 1) * TKS + tid) * 32] = 0u;
+        if (s_lim < nlist) {
+            tkc = P.tickets + ((it & 1) * TKS + tk_k) * 32;
+            if (wg0 && tid < TKS) {  // counter tid hands out slots s_lim + tid + TKS t < nlist
+                const int rem = nlist - s_lim - tid;
+                P.tickets[((it & 1) * TKS + tid) * 32 + 1] = rem > 0 ? (uint32_t)((rem + TKS - 1) / TKS) : 0u;
+            }
+        }
     }
     uint32_t tk_pend = 0;  // the ticket taken ahead (lane 0)
     // candidate update shared by every mode: Devex key, then the argmin
@@ -892,6 +902,19 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // workgroup argmin over waves (lane 0 of each wave holds the wave's best)
     if (lane == 0) red[wave] = PricePartial{best, bj, bw, be};
     __syncthreads();
+    if constexpr (DYN) {
+        // the previous pass's tickets (final: it ended at the kernel
+        // boundary): every wave draws from its counter until it gets a slot
+        // past the list, so a counter with waves ends above the slots it
+        // hands out; one below them had slots nobody priced (a wrong entering
+        // column, or a wrong optimum): stop loudly.  Then zero them.
+        if (P.price_dyn && wg0 && tid < TKS) {
+            uint32_t* o = P.tickets + (((it + 1) & 1) * TKS + tid) * 32;
+            if (o[1] > o[0]) st->uncovered = 1u;
+            o[0] = 0u;
+            o[1] = 0u;
+        }
+    }
     if (P.stamps && tid == 0 && blockIdx.x < 4096) {  // diagnostics: this workgroup's start and end
         unsigned long long* pw = P.stamps + STAMP_PRICE + (it & 1) * 4 * 4096 + 4 * (int64_t)blockIdx.x;
         pw[0] = t_pw0;
@@ -3087,6 +3110,7 @@ __global__ void k_reset(Params P) {
         st->nw = 0;
         st->leave = -1;
         st->wp = 1.0;
+        st->uncovered = 0u;
     }
 }
 

@@ -12,6 +12,13 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libsimplex's HIP path)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "run_last: long whole solves, moved to the end of the run")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    # the full-size C4 / C5 certificates (minutes) run after everything else,
+    # so a failure elsewhere shows up first under -x
+    items.sort(key=lambda it: 1 if it.get_closest_marker("run_last") else 0)
 
 
 @pytest.fixture(scope="session")

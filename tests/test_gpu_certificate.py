@@ -5,24 +5,30 @@ the optimum certified without any other solver (VERDICT r04
 container, tests/test_gpu_c4_optimum.py).
 
 The certificate is recomputed on the CPU in fp64 from the generator's A
-(oracle.generate: the checker, not the product) and the state the GPU hands
-back (basis, x_B, y):
-- primal feasibility: ||B x_B - b||_inf <= 1e-9 ||b||_inf and x_B >= 0;
-- dual feasibility: every reduced cost e_j = y.A_j - c_j >= -eps (the
-  solver's own optimality test, eps = 1e-7, v4:299-302) up to 1e-9 of
-  rounding, and |e_j| <= 1e-9 on the basic columns (y = c_B B^-1);
-- strong duality: b.y = c_B.x_B = z within 1e-9 (relative).
-A feasible basis whose duals are feasible is optimal, so z is the optimum.
-C4: 35,574 pivots in about 23 s.  C5 takes 137,499 pivots (about 141 s), so
-it runs only with SPX_LONG_TESTS=1; its round-5 run is profiles/r05_certificate.txt.
+(oracle.generate: the checker, not the product) and the basis the GPU hands
+back; the duals are recomputed on the CPU from that basis, not taken from the
+GPU:
+- primal feasibility: ||B x_B - b||_inf <= 1e-9 ||b||_inf and x_B >= 0, with
+  x_B the GPU's;
+- dual feasibility: y solves B^T y = c_B (numpy LU on the CPU) and every
+  reduced cost e_j = y.A_j - c_j is >= -eps_j, where eps_j is the solver's
+  own optimality tolerance (eps = 1e-7, v4:299-302, plus 1e-9 of rounding).  The test reports
+  min_j e_j, the largest dual infeasibility that remains;
+- the objective: z = c_B.x_B within 1e-9 (relative) of the GPU's z.
+This is an eps-optimality certificate, not an exact one: for every feasible
+x, c.x = b.y - sum_j e_j x_j <= b.y + delta * sum_j x_j with
+delta = max(0, -min_j e_j).  b.y = c_B.x_B holds for any basis (it is a
+consistency check, not optimality); what certifies is dual feasibility, and
+the test prints delta * sum(x_B), the bound's value at the solution.
+C4: 35,574 pivots in about 23 s; C5: 137,499 pivots in about 141 s.  Both run
+in the default GPU suite; conftest.py moves them to the end of the run.
 """
-import os
 import time
 
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
 
 EPS = 1e-7
 
@@ -36,23 +42,30 @@ def _certify(spx, oracle, m, n, seed):
     assert r.status == spx.SolveStatus.OptimumFound
     A, b, c = oracle.generate(m, n, seed)  # (n, m): row j = column j of A
     bix = np.asarray(s["b_ixs"], dtype=np.int64)
-    x_b, y = np.asarray(s["x_b"]), np.asarray(s["y"])
+    x_b = np.asarray(s["x_b"])
     assert len(set(bix.tolist())) == m
+    B = np.ascontiguousarray(A[bix].T)  # m x m basis matrix
     # primal: B x_B = b, x_B >= 0
-    res = A[bix].T @ x_b - b
+    res = B @ x_b - b
     assert np.max(np.abs(res)) <= 1e-9 * np.max(np.abs(b)), np.max(np.abs(res))
     assert np.min(x_b) >= -1e-9 * np.max(np.abs(x_b)), np.min(x_b)
-    # dual: e_j = y.A_j - c_j >= -eps for every column, ~0 on the basis
+    # dual: y from the basis on the CPU (B^T y = c_B), then e_j = y.A_j - c_j
+    y = np.linalg.solve(B.T, c[bix])
+    del B
+    y_gpu = np.asarray(s["y"])
+    dy = float(np.max(np.abs(y - y_gpu)))
+    assert dy <= 1e-6 * max(1.0, float(np.max(np.abs(y)))), dy  # the GPU's incrementally updated y
     e = A @ y - c
     del A
-    assert np.min(e) >= -EPS - 1e-9, np.min(e)
+    assert np.min(e) >= -EPS - 1e-9, np.min(e)  # (1e-9: rounding between the GPU's y and the CPU's)
     assert np.max(np.abs(e[bix])) <= 1e-9 * max(1.0, np.max(np.abs(c))), np.max(np.abs(e[bix]))
-    # strong duality
+    # the objective, and the eps-optimality bound at the solution
     z_p = float(c[bix] @ x_b)
-    z_d = float(b @ y)
-    assert abs(z_p - r.z) <= 1e-9 * abs(r.z) and abs(z_d - r.z) <= 1e-9 * abs(r.z), (z_p, z_d, r.z)
+    assert abs(z_p - r.z) <= 1e-9 * abs(r.z), (z_p, r.z)
+    delta = max(0.0, -float(np.min(e)))
     print(f"m={m} n={n}: {r.pivots} pivots in {t1 - t0:.1f} s, z={r.z:.15g}, "
-          f"primal residual {np.max(np.abs(res)):.2e}, min reduced cost {np.min(e):.2e}, b.y={z_d:.15g}")
+          f"primal residual {np.max(np.abs(res)):.2e}, min reduced cost {np.min(e):.2e} "
+          f"(CPU duals; GPU y within {dy:.1e}), delta*sum(x_B) = {delta * float(np.sum(x_b)):.2e}")
     return r
 
 
@@ -60,7 +73,5 @@ def test_c4_optimum_certified(spx, oracle):
     _certify(spx, oracle, 4096, 131072, 0)
 
 
-@pytest.mark.skipif(os.environ.get("SPX_LONG_TESTS") != "1",
-                    reason="137,499 pivots in about 141 s: SPX_LONG_TESTS=1 (run in round 5: profiles/r05_certificate.txt)")
 def test_c5_optimum_certified(spx, oracle):
     _certify(spx, oracle, 16384, 65536, 0)

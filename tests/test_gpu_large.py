@@ -176,3 +176,28 @@ def test_dynamic_pricing_tail_small_grids(spx, monkeypatch, grid):
     assert np.array_equal(tpa, tpb) and np.array_equal(tqa, tqb)
     for key in ("b_ixs", "x_b", "y"):
         assert np.array_equal(sa[key], sb[key]), key
+
+
+def test_ticketed_tail_unpriced_slots_fail_loudly(spx, monkeypatch):
+    """the ticketed tail's coverage is checked on the
+    device, not only by the host's cap.  A deliberately broken geometry -- 16
+    counters for one 8-wave pricing workgroup, the cap skipped
+    (SPX_TK_UNSAFE=1), so counters 8..15 have no wave drawing from them and
+    their slots go unpriced -- must stop the solve with an error
+    (SPX_ERR_STATE via DevState::uncovered or the host's last-pass check),
+    not return wrong pivots; the capped geometry on the same LP runs clean."""
+    m, n, seed = 300, 1200, 7
+    monkeypatch.setenv("SPX_PRICE_DYN", "2")
+    monkeypatch.setenv("SPX_TK_SHARDS", "16")
+    with spx.Context(m=m, n=n, seed=seed, window=16, persist=False, price_grid=1) as ctx:
+        st, piv = ctx.iterate(40)  # (capped: 8 counters, every one drawn from)
+        assert piv == 40
+    monkeypatch.setenv("SPX_TK_UNSAFE", "1")
+    with spx.Context(m=m, n=n, seed=seed, window=16, persist=False, price_grid=1) as ctx:
+        with pytest.raises(spx.SimplexError, match="unpriced"):
+            ctx.iterate(40)
+        with pytest.raises(spx.SimplexError, match="unpriced"):  # sticky until a reset
+            ctx.iterate(1)
+        monkeypatch.delenv("SPX_TK_UNSAFE")
+        ctx.reset()
+        ctx.iterate(0)  # (the flag is cleared; the context's counters are still 16)
