@@ -368,8 +368,10 @@ int spx_fold_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
  * ratio-test tail reduced, the staging in LDS (4 price grid values); then
  * the tick at which the FTRAN tail had issued the pivot's
  * bookkeeping (1 value), then the tick at which the diagnostic one-wave
- * kernel launched before the FTRAN pass started (SPX_DIAG_MARK=1; 1 value).
- * Copies min(cap, 2 (4 grid + 4 price grid + 2)) values; *count = grid. */
+ * kernel launched before the FTRAN pass started (SPX_DIAG_MARK=1; 1 value),
+ * then the tick k_price's workgroup 0 had issued the deferred tail's
+ * bookkeeping (1 value).
+ * Copies min(cap, 2 (4 grid + 4 price grid + 3)) values; *count = grid. */
 int spx_wg_times(spx_ctx* ctx, uint64_t* out, int64_t cap, int64_t* count);
 
 /* With SPX_FLAG_TIMING and the persistent loop kernel (spx_config out[8]

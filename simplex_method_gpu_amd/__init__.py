@@ -341,10 +341,11 @@ class Context:
         list in LDS / partial published, "price": (price grid, 4) start / end
         of the column loop / deferred tail reduced / staging in LDS, "tail": the tick the FTRAN tail had issued the
         bookkeeping, "mark": the start of the SPX_DIAG_MARK=1 probe kernel
-        launched before the FTRAN pass (0 without it)}."""
+        launched before the FTRAN pass (0 without it), "book": the tick k_price's
+        workgroup 0 had issued the deferred tail's bookkeeping}."""
         cfg = self.config()
         g, gp = cfg["update_grid"], cfg["price_grid"]
-        per = 4 * min(g, 4096) + 4 * min(gp, 4096) + 2
+        per = 4 * min(g, 4096) + 4 * min(gp, 4096) + 3
         out = np.zeros(2 * per, dtype=np.uint64)
         cnt = ctypes.c_int64()
         check(self._L.spx_wg_times(self._h, _ptr(out), out.size, ctypes.byref(cnt)))
@@ -353,7 +354,7 @@ class Context:
             b = out[par * per: (par + 1) * per]
             nu, npr = 4 * min(g, 4096), 4 * min(gp, 4096)
             res.append({"ftran": b[:nu].reshape(-1, 4), "price": b[nu: nu + npr].reshape(-1, 4),
-                        "tail": int(b[nu + npr]), "mark": int(b[nu + npr + 1])})
+                        "tail": int(b[nu + npr]), "mark": int(b[nu + npr + 1]), "book": int(b[nu + npr + 2])})
         return res
 
     def fold_times(self):

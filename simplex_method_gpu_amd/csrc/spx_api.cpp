@@ -1575,7 +1575,8 @@ int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
     if (!x || !out) return fail(SPX_ERR_ARG, "NULL argument");
     if (!x->P.stamps) return fail(SPX_ERR_STATE, "context created without SPX_FLAG_STAMPS");
     HIP_TRY(hipStreamSynchronize(x->stream));
-    // per parity: k_ftran_bc 4 per workgroup, k_price 4 per workgroup, the tail end, k_mark
+    // per parity: k_ftran_bc 4 per workgroup, k_price 4 per workgroup, the tail end, k_mark,
+    // k_price workgroup 0's deferred bookkeeping issued
     const int64_t gu = std::min(x->ucfg.grid, 4096), gp = std::min(x->pcfg.grid, 4096);
     std::vector<uint64_t> h((size_t)STAMP_WORDS);
     HIP_TRY(hipMemcpy(h.data(), x->P.stamps, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost));
@@ -1585,6 +1586,7 @@ int spx_wg_times(spx_ctx* x, uint64_t* out, int64_t cap, int64_t* count) {
         for (int64_t i = 0; i < 4 * gp && k < cap; ++i) out[k++] = h[(size_t)(STAMP_PRICE + par * 4 * 4096 + i)];
         if (k < cap) out[k++] = h[(size_t)(STAMP_TAIL + par)];
         if (k < cap) out[k++] = h[(size_t)(STAMP_TAIL + 2 + par)];
+        if (k < cap) out[k++] = h[(size_t)(STAMP_TAIL + 4 + par)];
     }
     if (count) *count = x->ucfg.grid;
     return SPX_OK;

@@ -72,6 +72,12 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 #ifndef SPX_BC_PF
 #define SPX_BC_PF 1  // C3 A/B (tools/r02_abbench.sh): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
 #endif
+#ifndef SPX_FTRAN_TRIM
+// k_ftran_bc's entry loads (A/B): 1 = the compact row's chunk 0 only up to S
+// (lanes past it re-read the row's first line), 2 = the U row only up to the
+// window's pending pivots (requested after the state arrives)
+#define SPX_FTRAN_TRIM 0
+#endif
 #ifndef SPX_BC_PF2
 #define SPX_BC_PF2 4
 #endif
@@ -256,9 +262,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // its own staging loads: vmcnt retires in order)
     __shared__ TailRec s_rec;
     __shared__ UpdPartial s_tp;
-#if defined(SPX_DIAG_FETCH_STAMP) || defined(SPX_DIAG_MERGE_STAMP)
-    unsigned long long t_fetch_all = 0;
-#endif
     if (DT && P.defer_tail) {
         fresh = R.fresh != 0;
         if constexpr (DEEP) {
@@ -293,15 +296,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         }
         if (fresh) {
             __shared__ UpdPartial s_ured[(PAIR ? 2 * WAVES : WAVES) + 1];
-#ifdef SPX_DIAG_FETCH_STAMP  // timing probe: when the partials have arrived (stored as the pw[3] clock)
-            {
-                const int g0 = tid < P.tail_parts ? tid : 0;
-                const double th0 = P.upd_soa[g0];
-                const double bx0 = P.upd_soa[6 * P.upd_cap + g0];
-                asm volatile("" ::"v"(th0), "v"(bx0));
-                t_fetch_all = rtime();
-            }
-#endif
             UpdPartial t;
             if constexpr (PAIR) {
                 for (int g = tid + 2 * BLOCK; g < P.tail_parts; g += 2 * BLOCK) {
@@ -311,13 +305,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 t = reduce_partial_pair<BLOCK>(w0, w1, s_ured);
             } else {
                 for (int g = tid + BLOCK; g < P.tail_parts; g += BLOCK) upd_merge(w0, upd_fetch<true>(P, g));
-#ifdef SPX_DIAG_MERGE_STAMP  // timing probe: the wave reductions alone, then the merge (pw[3] / pw[2])
-                {
-                    const UpdPartial o = wave_reduce_partial(w0);
-                    asm volatile("" ::"v"(o.theta), "v"(o.T));
-                    t_fetch_all = rtime();
-                }
-#endif
                 t = reduce_partial_block<BLOCK, true>(w0, s_ured);
             }
             const int64_t q = t.idx;
@@ -920,16 +907,15 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         pw[0] = t_pw0;
         pw[1] = rtime();
         pw[2] = t_pw1;
-#if defined(SPX_DIAG_FETCH_STAMP) || defined(SPX_DIAG_MERGE_STAMP)
-        pw[3] = t_fetch_all;
-#else
         pw[3] = t_pw2;
-#endif
     }
     if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
         if (tid == 0) {
             P.price_partials[blockIdx.x] = red[best_wave<WAVES>(red)];
-            if (fresh && blockIdx.x == 0) apply_deferred_tail(P, st, s_rec, s_tp);
+            if (fresh && blockIdx.x == 0) {
+                apply_deferred_tail(P, st, s_rec, s_tp);
+                if (P.stamps) P.stamps[STAMP_TAIL + 4 + (it & 1)] = rtime();  // the bookkeeping is issued
+            }
         }
         return;
     }
@@ -2202,7 +2188,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
         cbv[r] = P.c_B[icl[r]];
         xb0[r] = P.x_b[icl[r]];
         bix[r] = P.b_ixs[icl[r]];
-        urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
+        if constexpr (!(SPX_FTRAN_TRIM & 2)) urow[r] = P.U[icl[r] * KW + (lane < KW ? lane : 0)];
     }
     const double sxw_w = P.Wt[P.n * KW + (lane < KW ? lane : 0)];
     struct {
@@ -2233,9 +2219,14 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
 #pragma unroll
         for (int t = 0; t < NCH; ++t) {
             const int k2 = lane + 64 * t;
-            const int kk = t == 0 ? (k2 < L2 ? k2 : (int)L2 - 1) : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
+            const int kk = t == 0 ? ((SPX_FTRAN_TRIM & 1) ? (2 * k2 < Sbc ? k2 : 0) : (k2 < L2 ? k2 : (int)L2 - 1))
+                                  : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
             pf[r][t] = brow[r][kk];
         }
+    }
+    if constexpr ((SPX_FTRAN_TRIM & 2) != 0) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) urow[r] = P.U[icl[r] * KW + (lane < Sv.nw - 1 ? lane : 0)];
     }
     const int64_t qp = Sv.q;
     const bool pend = Sv.nw > 0;
@@ -2392,9 +2383,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
         }
         for (int c = cb + (cb == 0 ? BC_RL * BLOCK : 0) + tid; c < ce; c += BLOCK) apc[c - cb] = apd[P.rlist[c]];
         lds_barrier();
-#ifndef SPX_DIAG_FTRAN_SUM
         if (wgt && cb == 0) wgt[2] = rtime();
-#endif
         const int kb = cb >> 1, ke = (ce + 1) >> 1;  // this block's dbl2 chunks
 #pragma unroll
         for (int r = 0; r < RPW; ++r) {
@@ -2461,12 +2450,6 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     rows_step(std::integral_constant<int, 4>());
     rows_step(std::integral_constant<int, 2>());
     rows_step(std::integral_constant<int, 1>());
-#ifdef SPX_DIAG_FTRAN_SUM  // timing probe: clock 2 = the row sums are done (in place of A_p in LDS)
-    if (wgt) {
-        asm volatile("" ::"v"(acc[0]), "v"(sxw));
-        wgt[2] = rtime();
-    }
-#endif
     UpdPartial wp[RPW];
     double al[RPW], xb[RPW];
 #pragma unroll

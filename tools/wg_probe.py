@@ -48,24 +48,18 @@ with spx.Context(m=a.m, n=a.n, seed=0, device=0, stamps=True, **kw) as ctx:
         f0 = fa[:, 0].min()
         put("price_entry_spread", pa[:, 0].max() - p0)
         put("price_entry_to_tail_reduced", np.median(pa[:, 2] - pa[:, 0]))
-        if os.environ.get("SPX_LIB", "").find("xfst") >= 0:  # (build with SPX_DIAG_FETCH_STAMP: clock 3 = partials in)
-            put("price_entry_to_partials_in", np.median(pa[:, 3] - pa[:, 0]))
-        elif os.environ.get("SPX_LIB", "").find("xmrg") >= 0:  # (SPX_DIAG_MERGE_STAMP: clock 3 = wave reductions done)
-            put("price_entry_to_wave_reduced", np.median(pa[:, 3] - pa[:, 0]))
-        else:
-            put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
+        put("price_tail_reduced_to_staged", np.median(pa[:, 3] - pa[:, 2]))
         put("price_span", pa[:, 1].max() - p0)
         put("price_end_spread", pa[:, 1].max() - pa[:, 1].min())
         put("wg0_end_minus_p50_end", pa[0, 1] - np.median(pa[:, 1]))
         put("price_end_to_ftran_entry", f0 - pa[:, 1].max())
+        if A["book"] > 0:  # workgroup 0's deferred bookkeeping, after its columns
+            put("wg0_bookkeeping_issued_minus_last_end", int(A["book"]) - pa[:, 1].max())
+            put("wg0_end_to_bookkeeping_issued", int(A["book"]) - pa[0, 1])
         put("ftran_entry_spread", fa[:, 0].max() - f0)
         put("ftran_entry_to_p", np.median(fa[:, 1] - fa[:, 0]))
-        if os.environ.get("SPX_LIB", "").find("xfsum") >= 0:  # (SPX_DIAG_FTRAN_SUM: clock 2 = row sums done)
-            put("ftran_p_to_sums_done", np.median(fa[:, 2] - fa[:, 1]))
-            put("ftran_sums_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
-        else:
-            put("ftran_p_to_ap_lds", np.median(fa[:, 2] - fa[:, 1]))
-            put("ftran_ap_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
+        put("ftran_p_to_ap_lds", np.median(fa[:, 2] - fa[:, 1]))
+        put("ftran_ap_to_publish_p50", np.median(fa[:, 3] - fa[:, 2]))
         put("ftran_publish_max", fa[:, 3].max() - f0)
         if A["tail"] > fa[:, 3].max():  # the FTRAN pass ran the tail itself
             put("publish_max_to_tail", int(A["tail"]) - fa[:, 3].max())

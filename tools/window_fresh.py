@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--nw", type=int, default=10)
     ap.add_argument("--pre", default="none")
+    ap.add_argument("--shift", type=int, default=0, help="untimed whole windows before the first timed one")
     a = ap.parse_args()
     import torch
     import simplex_method_gpu_amd as spx
@@ -33,8 +34,9 @@ def main():
             c.iterate(200)
     elif a.pre == "idle":
         time.sleep(2.0)
-    res = run(spx, torch, m, n, steps, 5, a.nw)
-    print(json.dumps({"config": a.config, "pre": a.pre, "it_s": [r["it_s"] for r in res],
+    res = run(spx, torch, m, n, steps, 5, a.nw, shift=a.shift)
+    print(json.dumps({"config": a.config, "pre": a.pre, "shift": a.shift, "it_s": [r["it_s"] for r in res],
+                      "price_MB_end": [r["price_MB"] for r in res],
                       "piv0": [r["piv0"] for r in res], "S": [r["S"] for r in res],
                       "wall_s": round(time.time() - t0, 2)}), flush=True)
 

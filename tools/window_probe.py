@@ -53,7 +53,9 @@ def run(spx, torch, m, n, steps_req, warmup, nw, shift=0, sleep=0.0, prime=0, st
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         d1 = ctx.dispatch_stats()
+        inf = ctx.info()
         out.append({"it_s": round((p1 - piv) / dt, 1), "piv0": piv, "S": ctx.ftran_cols(),
+                    "price_MB": round(inf["bytes_price"] / 1e6, 2),
                     "graphs": d1["graph_launches"] - d0["graph_launches"],
                     "eager": d1["eager_passes"] - d0["eager_passes"], "folds": d1["folds"] - d0["folds"]})
         piv = p1
