@@ -11,8 +11,9 @@ B^-1 is kept in the representation the library picks for (m, n) — the eta
 window of 64 (B_w + U R) at m >= 2048 (C3, C4, C5), the explicit
 inverse at C2 — at every N.  The window's rank-63 fold runs every 63 pivots, so
 the timed region is aligned to whole windows — W untimed warm-up pivots, then untimed pivots up to the next window
-boundary, then K rounded up to a multiple of 63 timed pivots, which therefore
-hold exactly K/63 folds (`timed_region` reports the pivots, folds and hipGraph
+boundary, then K rounded up to a multiple of 63 timed pivots -- at least
+MIN_SPAN = 252 (four windows, about 19 ms at C3), so no single window's
+transient sets the rate -- which therefore hold exactly K/63 folds (`timed_region` reports the pivots, folds and hipGraph
 replays the library enqueued there, and `config.dispatch` is derived from
 those counts).  `explicit` times the reference's own representation (explicit
 B^-1 rewritten by a rank-1 update every pivot, v4:331-333) on the same LP with
@@ -124,6 +125,18 @@ class Watchdog:
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# The shortest timed span, in pivots (rounded up to whole windows / batches).
+# One 63-pivot window measured 0.4-1.6 % below the windows after it in bench
+# runs (tools/window_probe.py, window_fresh.py: the first window after the
+# warm-up streams slightly more pricing bytes -- fewer slack columns have left
+# the basis -- and is the first replay timed); four windows make the rate
+# representative of the sustained one (timed_region.next_windows_it_per_s).
+MIN_SPAN = 252
+
+
+def span(k, per):
+    """K pivots rounded up to whole units of `per`, at least MIN_SPAN."""
+    return per * max(-(-k // per), -(-MIN_SPAN // per), 1)
 CONFIGS = {"C2": (1024, 4096), "C3": (4096, 16384), "C4": (4096, 131072), "C5": (16384, 65536)}
 METRIC = "simplex iterations/sec on dense m={m} n={n} fp64; achieved HBM GB/s"  # BASELINE.json at C3
 
@@ -278,7 +291,7 @@ def main():
         # (explicit B^-1: the timed region replays graphs, as the window's does)
         per = kw - 1 if kw else max(cfg["graph_batch"], 1)
         warm = per
-        steps = per * max(1, -(-args.steps // per))
+        steps = span(args.steps, per)
         ctx.iterate(args.warmup)
         lead = 0
         if kw:
@@ -485,8 +498,9 @@ def main():
             },
             "timed_region": {
                 "pivots": main_run["pivots"],
-                "steps_rounding": (f"K rounded up to whole windows of {win - 1} pivots" if win else
-                                   f"K rounded up to whole captured batches of {cfg['graph_batch']} passes"
+                "steps_rounding": ((f"K rounded up to whole windows of {win - 1} pivots" if win else
+                                    f"K rounded up to whole captured batches of {cfg['graph_batch']} passes")
+                                   + f", at least {MIN_SPAN} pivots (one window's transient does not set the rate)"
                                    if cfg["graph_batch"] > 0 else "none"),
                 "untimed_pivots_before": args.warmup + main_run["lead"],
                 "folds": main_run["dispatch"]["folds"],
@@ -624,7 +638,7 @@ def steepest_block(spx, torch, m, n, args, device):
                          timing=timing) as ctx:
             cfg = ctx.config()
             per = max(cfg["window"] - 1, 1)
-            steps = per * max(1, -(-args.steps // per))
+            steps = span(args.steps, per)
             ctx.iterate(args.warmup)
             ds = ctx.dispatch_stats()
             if ds["window"] and ds["window_pos"] < ds["window"]:
@@ -744,7 +758,7 @@ def tableau_block(spx, torch, m, n, args, device):
         with spx.Context(m=m, n=n, seed=args.seed, device=device, timing=timing, tableau=True) as ctx:
             cfg = ctx.config()
             per = max(cfg["window"] - 1, 1)
-            steps = per * max(1, -(-args.steps // per))
+            steps = span(args.steps, per)
             ctx.iterate(args.warmup)
             ds = ctx.dispatch_stats()
             if ds["window"] and ds["window_pos"] < ds["window"]:

@@ -53,6 +53,12 @@ namespace spx {
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
+#ifndef SPX_PRICE_DEEP1
+#define SPX_PRICE_DEEP1 0  // (A/B, with SPX_PRICE_DEEP=0) WM 1 with the one-batch deep prefetch
+#endif
+#ifndef SPX_PRICE_DEEP_SE
+#define SPX_PRICE_DEEP_SE 0  // steepest edge (WM 4): the first column's first 8 chunks requested before it
+#endif
 #ifndef SPX_PRICE_DYN_PCT
 #define SPX_PRICE_DYN_PCT 85  // the share of the columns handed out statically (grid stride)
 #endif
@@ -73,10 +79,12 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 #define SPX_BC_PF 1  // C3 A/B (tools/r02_abbench.sh): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
 #endif
 #ifndef SPX_FTRAN_TRIM
-// k_ftran_bc's entry loads (A/B): 1 = the compact row's chunk 0 only up to S
-// (lanes past it re-read the row's first line), 2 = the U row only up to the
-// window's pending pivots (requested after the state arrives)
-#define SPX_FTRAN_TRIM 0
+// k_ftran_bc's entry loads: 2 = the U row only up to the window's pending
+// pivots, requested after the state arrives (the default since round 6: PMC
+// read per launch 5.27 -> 3.70 MB, C3 pass 74.76 -> 74.75 us, tools/ftran_ab.sh,
+// profiles/r06_ftran_ab.txt); 1 = the compact row's chunks only up to S as
+// well (lanes past it re-read the row's first line): 2.91 MB but 75.16 us
+#define SPX_FTRAN_TRIM 2
 #endif
 #ifndef SPX_BC_PF2
 #define SPX_BC_PF2 4
@@ -254,8 +262,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // shape): with the base row read from L2 (WM 2, C5) it measured 4.6 %
     // slower per pass (1,071 against 1,022 us, tools/pass_ab.py).
     // (only run_pipe consumes vd0 / vd1, so DEEP needs the pipelined loop)
-    constexpr bool DEEP = SPX_PRICE_DEEP && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8;
-    dbl2 vd0[DEEP ? CH : 1], vd1[DEEP ? CH : 1];
+    // (steepest edge, WM 4: its third dot leaves room for the first batch only,
+    // SPX_PRICE_DEEP_SE; two batches spilled)
+    constexpr bool DEEP2 = SPX_PRICE_DEEP && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8;
+    constexpr bool DEEP = DEEP2 || (SPX_PRICE_DEEP_SE && SPX_PRICE_PIPE && WM == 4 && BLOCK <= 512 && CH == 8) ||
+                          (SPX_PRICE_DEEP1 && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8);
+    dbl2 vd0[DEEP ? CH : 1], vd1[DEEP2 ? CH : 1];
     int64_t jdeep = -1;  // the column the deep prefetch holds (-1: none)
     // the bookkeeping's inputs for workgroup 0's thread 0, which applies them
     // after its columns (issued first, its stores would hold up the waits for
@@ -281,10 +293,12 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 const int64_t k = lane + u * 64;
                 vd0[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
             }
+            if constexpr (DEEP2) {
 #pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int64_t k = CH * 64 + lane + u * 64;
-                vd1[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
+                for (int u = 0; u < CH; ++u) {
+                    const int64_t k = CH * 64 + lane + u * 64;
+                    vd1[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
+                }
             }
             jdeep = dv ? jd : -1;
         }
@@ -704,7 +718,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             };
             int64_t kb = CH * 64;
             dbl2 vc[8];
-            if (DEEP && first && deep_hit) {
+            if (DEEP2 && first && deep_hit) {
                 // the two deep-prefetched batches, the third requested first
                 kb = 2 * CH * 64;
                 if (kb < L2) {
@@ -717,6 +731,11 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                     k = L2;
                     return;
                 }
+            } else if (DEEP && first && deep_hit) {
+                // (WM 4) the one deep-prefetched batch in place of v0
+#pragma unroll
+                for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
+                consume(vd0, CH, 0);
             } else {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) vc[u] = ld2<SPX_NT_A>(&col[kb + lane + u * 64]);
@@ -2219,8 +2238,8 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
 #pragma unroll
         for (int t = 0; t < NCH; ++t) {
             const int k2 = lane + 64 * t;
-            const int kk = t == 0 ? ((SPX_FTRAN_TRIM & 1) ? (2 * k2 < Sbc ? k2 : 0) : (k2 < L2 ? k2 : (int)L2 - 1))
-                                  : ((2 * k2 < Sbc && k2 < L2) ? k2 : lane);
+            const int kk = t == 0 ? ((SPX_FTRAN_TRIM & 1) ? (2 * k2 < Sbc ? k2 : (lane & 7)) : (k2 < L2 ? k2 : (int)L2 - 1))
+                                  : ((2 * k2 < Sbc && k2 < L2) ? k2 : ((SPX_FTRAN_TRIM & 1) ? (lane & 7) : lane));
             pf[r][t] = brow[r][kk];
         }
     }
