@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 7
+#define SPX_ABI_VERSION 8
 
 /* SolveStatus of the reference (v4_cub_reduction.cu:49-54), same numbering. */
 #define SPX_STATUS_MAX_ITER       0
@@ -403,8 +403,11 @@ int spx_info(spx_ctx* ctx, int64_t* m, int64_t* n, int64_t* ld,
  * window passes on one rank, SPX_DEFER_TAIL=0 turns it off) or run by the
  * FTRAN pass's last workgroup (0), [13] the window fold updates only B_w's
  * listed (non-unit) columns (1: k_cfold; SPX_DENSE_FOLD=1 turns it off) or
- * the dense B_w (0), [14] k_ftran_bc rows per wave (0: not in use). */
-#define SPX_CONFIG_FIELDS 15
+ * the dense B_w (0), [14] k_ftran_bc rows per wave (0: not in use), [15]
+ * (after spx_mbox_attach) loop passes exchange through the mailboxes inside
+ * k_price and k_ftran_bc (1: the fused exchange; SPX_MBOX_FUSED=0 turns it
+ * off) or with a k_exchange launch per pass (0). */
+#define SPX_CONFIG_FIELDS 16
 int spx_config(spx_ctx* ctx, int32_t out[SPX_CONFIG_FIELDS]);
 
 /* Columns of B^-1 the FTRAN stream reads per row: m, or with the eta window's

@@ -422,11 +422,11 @@ class Context:
 
     def config(self):
         """Resolved representation and launch geometry (spx_config)."""
-        out = (ctypes.c_int32 * 15)()
+        out = (ctypes.c_int32 * 16)()
         check(self._L.spx_config(self._h, out))
         keys = ("window", "price_block", "price_grid", "price_lds", "update_block", "update_rows", "update_grid",
                 "graph_batch", "persistent", "loop_block", "tableau", "loop_grid", "defer_tail", "compact_fold",
-                "ftran_rows_per_wave")
+                "ftran_rows_per_wave", "mbox_fused")
         return dict(zip(keys, list(out)))
 
 

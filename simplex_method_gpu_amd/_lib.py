@@ -10,7 +10,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SPX_LIB: alternative build of the same library (e.g. a cache-policy variant
-# from tools/policy_sweep.sh); default is the in-tree product build.
+# from a cache-policy sweep; tools/pass_ab.py); default is the in-tree product build.
 LIB_PATH = os.environ.get("SPX_LIB") or os.path.join(_HERE, "libsimplex.so")
 
 # symbol -> (restype, argtypes); mirrors include/simplex.h

@@ -111,6 +111,7 @@ struct spx_ctx {
     uint64_t** mbox_peer = nullptr;  // device array of nranks mailbox pointers
     std::vector<void*> mbox_opened;  // IPC mappings of the other ranks' mailboxes
     bool mbox_ready = false;
+    bool mbox_fused = false;  // loop passes exchange inside k_price / k_ftran_bc (Params::mbox_fused)
     bool bc_want = false;      // compact FTRAN operand wanted (allocated by set_slack_flags)
     bool slack_ident = false;  // A[:, n-m:] = I (checked before setup_common)
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
@@ -716,10 +717,11 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
     Pp.defer_price = x->defer_ok ? 1 : 0;
     Pp.defer_tail = x->defer_tail ? 1 : 0;
+    Pp.mbox_fused = (x->mbox_ready && x->mbox_fused) ? 1 : 0;
     HIP_TRY(launch_price(Pp, x->pcfg, x->stream, p0, p1));
     if (x->use_comm) {
         if (x->mbox_ready) {
-            HIP_TRY(launch_exchange(x->P, x->stream));
+            if (!Pp.mbox_fused) HIP_TRY(launch_exchange(x->P, x->stream));
         } else {
             if (!x->comm_ready) return fail(SPX_ERR_STATE, "nranks > 1 but neither spx_attach_comm nor spx_mbox_attach was called");
             NCCL_TRY(ncclAllGather(x->send, x->recv, sizeof(ArgMinEntry) * x->P.pr_stride, ncclUint8, x->comm,
@@ -1159,7 +1161,7 @@ int set_slack_flags(spx_ctx* x) {
     // reduce_partial_pair), k_apply_tail and the FTRAN tail share -- on one rank
     // with the pricing tail deferred as well; with G ranks (replicated B_w, so
     // every rank holds the same FTRAN partials) the pricing tail stays in
-    // k_price for the exchange.  Measured at C3 (tools/fuse_est.py, the
+    // k_price for the exchange.  Measured at C3 (round-2 tools/fuse_est.py, in git history, the
     // timing-only estimate): 79.8 -> 73.9 us per pass.  SPX_DEFER_TAIL=0 keeps
     // the tail in the FTRAN pass.
     const UpdateCfg& uc = x->ucfg;
@@ -1334,6 +1336,7 @@ int spx_mbox_attach(spx_ctx* x, const uint8_t* handles) {
     HIP_TRY(hipSetDevice(x->device));
     const int G = x->opts.nranks;
     std::vector<uint64_t*> peers((size_t)G);
+    bool shared_device = false;  // a peer's mailbox on this context's own device (ranks sharing a GPU)
     for (int g = 0; g < G; ++g) {
         if (g == x->opts.rank) {
             peers[(size_t)g] = x->mbox;
@@ -1346,6 +1349,9 @@ int spx_mbox_attach(spx_ctx* x, const uint8_t* handles) {
         if (e != hipSuccess) return fail(SPX_ERR_HIP, "hipIpcOpenMemHandle(rank %d): %s", g, hipGetErrorString(e));
         x->mbox_opened.push_back(p);
         peers[(size_t)g] = static_cast<uint64_t*>(p);
+        hipPointerAttribute_t a{};
+        // (unknown counts as shared: the k_exchange path is safe everywhere)
+        if (hipPointerGetAttributes(&a, p) != hipSuccess || a.device == x->device) shared_device = true;
     }
     SPX_TRY(x->alloc(&x->mbox_peer, (size_t)G));
     HIP_TRY(hipMemcpyAsync(x->mbox_peer, peers.data(), sizeof(uint64_t*) * (size_t)G, hipMemcpyHostToDevice,
@@ -1355,6 +1361,16 @@ int spx_mbox_attach(spx_ctx* x, const uint8_t* handles) {
     x->P.mbox = x->mbox;
     x->P.mbox_seq = x->mbox_seq;
     x->P.mbox_rank = x->opts.rank;
+    // the fused exchange where the loop pass is k_price (tagged pricing tail)
+    // + k_ftran_bc (compact window FTRAN, one row per wave), and no peer
+    // shares this device: there, a rank's k_ftran_bc workgroups, spinning on
+    // the mailbox, can hold every CU a peer's k_price needs to produce the
+    // record (measured: two processes on one GPU at m = 2048 time out), so
+    // ranks sharing a GPU keep the one-workgroup k_exchange launch.
+    // SPX_MBOX_FUSED=0 keeps it everywhere
+    x->mbox_fused = x->P.win && x->P.bc && x->P.price_tag && !x->P.row_shard && !x->P.split_tail &&
+                    x->ucfg.rows == 1 && x->ucfg.bc_entry && G <= 64 && !shared_device &&
+                    !env_off("SPX_MBOX_FUSED");
     // a graph captured before (with the RCCL exchange, or none) is rebuilt
     if (x->graph_exec) (void)hipGraphExecDestroy(x->graph_exec);
     if (x->graph) (void)hipGraphDestroy(x->graph);
@@ -1909,6 +1925,7 @@ int spx_config(spx_ctx* x, int32_t out[SPX_CONFIG_FIELDS]) {
     out[12] = x->defer_tail ? 1 : 0;
     out[13] = (x->P.bc && x->P.cfold) ? 1 : 0;
     out[14] = (x->P.bc && x->ucfg.rows == 1 && x->ucfg.bc_entry) ? x->ucfg.bc_entry : 0;
+    out[15] = (x->mbox_ready && x->mbox_fused) ? 1 : 0;
     return SPX_OK;
 }
 

@@ -16,7 +16,7 @@ namespace spx {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
-// Cache policy of the three big streams (compile-time; tools/policy_sweep.sh
+// Cache policy of the three big streams (compile-time; round-1/2 tools/policy_sweep.sh, in git history
 // builds the variants): 1 = non-temporal, 0 = default.  Measured at C3:
 // non-temporal loads of A cut k_price 93 -> 68 us, of B^-1 k_update 69 -> 56 us.
 #ifndef SPX_NT_A
@@ -32,7 +32,7 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 // while B_w is at most SPX_BWIN_CACHED bytes, non-temporal beyond.  B_w is
 // rewritten by k_fold's default-policy stores and read back every pass between
 // A streams loaded non-temporally, so a B_w that fits the 256 MiB Infinity
-// Cache stays partly resident.  Measured (tools/policy_win.sh, r02_bwin.sh):
+// Cache stays partly resident.  Measured (round-2 tools/policy_win.sh and r02_bwin.sh, in git history):
 // C3 (134 MB) k_update 31.8 us nt -> 28.0 us default; C5 (2.1 GB, two-kernel
 // passes) 352-360 us nt against 383-410 us default.
 #ifndef SPX_BWIN_CACHED

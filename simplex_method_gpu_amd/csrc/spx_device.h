@@ -156,7 +156,7 @@ struct alignas(16) DevState {
     int64_t xb_applied;  // x_b includes the first xb_applied pivots
     int32_t y_buf;
     uint32_t pad_t0;     // (the arrival counters live in Params::arrive)
-    uint32_t pad_t1;
+    uint32_t mbox_epoch;  // fused mailbox exchange: the tags' high byte, advanced by every reset
     int32_t nw;          // eta window: pivots since the last fold (nw-1 pending)
     uint32_t uncovered;  // set by k_price: a pass's ticketed list slots were not all taken (never cleared but by a reset)
     int32_t pad1;
@@ -312,6 +312,11 @@ struct Params {
     uint64_t* mbox;
     uint32_t* mbox_seq;
     int32_t mbox_rank;
+    // fused exchange (loop passes of a compact window, set per launch by
+    // enqueue_pass): k_price's pricing tail stores the record into every
+    // rank's mailbox itself and k_ftran_bc polls its own -- no k_exchange
+    // launch.  Tags: (mbox_epoch << 24) | (iteration + 1), parity iteration & 1
+    int32_t mbox_fused;
     // A[:, ns:] = I exactly (checked at create; SPX_DENSE_SLACKS=1 turns it
     // off): k_price prices a non-basic slack column without streaming it
     int32_t slack_unit;

@@ -76,7 +76,7 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 // k_update entry (256 columns), and column-list entries per thread requested
 // ahead of the entering column (1,024 columns at 512 threads)
 #ifndef SPX_BC_PF
-#define SPX_BC_PF 1  // C3 A/B (tools/r02_abbench.sh): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
+#define SPX_BC_PF 1  // C3 A/B (round-2 tools/r02_abbench.sh, in git history): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
 #endif
 #ifndef SPX_FTRAN_TRIM
 // k_ftran_bc's entry loads: 2 = the U row only up to the window's pending
@@ -174,6 +174,39 @@ __device__ __forceinline__ int best_wave(const PricePartial* red) {
 // stream, each column reads T_w[q_tau, j], dw[j] and its Wt row; 4 / 5 = 1 / 2
 // with steepest-edge pricing (P.steep): a third dot v.A_j per column, v =
 // B_w^T alpha (P.se_v) in LDS beside y and the base row (4) or from global (5).
+// Peer mailboxes (k_exchange below; the fused exchange in k_price's pricing
+// tail and k_ftran_bc's entry).  A rank that polls for MBOX_TIMEOUT_TICKS
+// without seeing a peer's word stops with ST_HANDOFF_TIMEOUT.
+constexpr unsigned long long MBOX_TIMEOUT_TICKS = 3000000000ull;  // 30 s of s_memrealtime (100 MHz)
+constexpr int MBOX_FUSED_MAX_G = 64;  // ranks the fused receiver merges (k_ftran_bc LDS)
+// Fused exchange (Params::mbox_fused): a loop pass's record carries the tag
+// (epoch << 24) | (iteration + 1) in every word; the epoch (DevState,
+// advanced by every reset on every rank) keeps a record of an earlier solve
+// from matching after the iteration count restarts.  k_exchange's seq tags
+// stay below 2^24, so the two never match each other's words.
+__device__ __forceinline__ uint32_t mbox_tag(uint32_t epoch, int64_t it) {
+    return (epoch << 24) | ((uint32_t)(it + 1) & 0xFFFFFFu);
+}
+// word h of rank g's record in this rank's mailbox, polled until it carries tag
+__device__ __forceinline__ bool mbox_poll(const Params& P, int64_t par, int g, int h, uint32_t tag,
+                                          uint32_t* half) {
+    const int64_t nh = (int64_t)P.pr_stride * 4;
+    const uint64_t* q = &P.mbox[(par * P.nin + g) * nh + h];
+    const unsigned long long t0 = rtime();
+    for (;;) {
+        const uint64_t w = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(w >> 32) == tag) {
+            *half = (uint32_t)w;
+            return true;
+        }
+        if (rtime() - t0 > MBOX_TIMEOUT_TICKS) {
+            *half = 0u;
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 template <int BLOCK, bool PLAIN = false>
 __device__ UpdPartial reduce_update_partials(const Params& P, UpdPartial* red, int nparts, uint32_t tag = 0,
                                              bool* timed_out = nullptr);
@@ -1024,6 +1057,34 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             double* wo = reinterpret_cast<double*>(P.price_out + 1);
             if (tid < KW)
                 wo[tid] = (t.idx == INT64_MAX || tid >= nw) ? 0.0 : (tid == tau ? t.w : P.Wt[t.idx * KW + tid]);
+        }
+        if (WIN && P.mbox_fused) {
+            // fused exchange: the record (the same words k_exchange would
+            // send: the entry, the winner's window coefficients, Devex's
+            // reduced cost and weight) stored into every rank's mailbox
+            // straight from here, one 32-bit half per thread and word
+            const int nh = P.pr_stride * 4;
+            const int G = P.nin;
+            const uint32_t tag = mbox_tag(S.mbox_epoch, it);
+            const int64_t par = it & 1;
+            for (int h = tid; h < nh; h += BLOCK) {
+                const int f = h >> 1;  // the record's 8-byte field
+                uint64_t u;
+                if (f == 0) u = (uint64_t)__double_as_longlong(t.val);
+                else if (f == 1) u = (uint64_t)t.idx;
+                else if (f < 2 + KW) {
+                    const int d = f - 2;
+                    const double v = (t.idx == INT64_MAX || d >= nw) ? 0.0 : (d == tau ? t.w : P.Wt[t.idx * KW + d]);
+                    u = (uint64_t)__double_as_longlong(v);
+                } else {
+                    const double v = f == 2 + KW ? t.pad : (t.idx == INT64_MAX ? 1.0 : ld_agent(&P.W[t.idx]));
+                    u = (uint64_t)__double_as_longlong(v);
+                }
+                const uint64_t w = ((uint64_t)tag << 32) | ((h & 1) ? (uint32_t)(u >> 32) : (uint32_t)u);
+                for (int g = 0; g < G; ++g)
+                    __hip_atomic_store(&P.mbox_peer[g][(par * G + P.mbox_rank) * nh + h], w, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
         stamp_tail(slot, t_tail, win);
         return;
@@ -2258,6 +2319,11 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     double min_e = INFINITY, e_enter = 0.0;
     int64_t p = INT64_MAX;
     int gw = 0;
+    // (fused exchange: the polled entries, the winner's record after its
+    // entry -- KW window coefficients, then Devex's two -- and a timeout flag)
+    __shared__ uint32_t s_fh[4 * MBOX_FUSED_MAX_G];
+    __shared__ double s_fw[64 + 2];
+    __shared__ int s_fto;
     if (P.defer_price) {
         PricePartial w = tid < P.price_grid ? pwl : PricePartial{INFINITY, INT64_MAX, 0.0, 0.0};
         for (int g = tid + BLOCK; g < P.price_grid; g += BLOCK) {
@@ -2303,6 +2369,52 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
             p = t.idx;
             e_enter = t.pad;
         }
+    } else if (P.mbox_fused) {
+        // fused exchange: wave 0 polls the ranks' entries in this rank's
+        // mailbox, every wave merges them (the same rule as the all-gather's
+        // consumers), then wave 0 polls the winner's window coefficients and
+        // Devex payload; both reach the other waves through LDS
+        const int G = P.nin;
+        const bool live = Sv.status == ST_RUNNING && Sv.iter < Sv.limit;
+        const uint32_t tag = mbox_tag(st->mbox_epoch, Sv.iter);
+        const int64_t par = Sv.iter & 1;
+        if (tid == 0) s_fto = 0;
+        if (wave == 0 && live) {
+            bool ok = true;
+            for (int k = lane; k < 4 * G; k += 64) {
+                uint32_t hf = 0u;
+                ok = mbox_poll(P, par, k >> 2, k & 3, tag, &hf) && ok;
+                s_fh[k] = hf;
+            }
+            if (!ok) s_fto = 1;  // (a benign race: every writer stores 1)
+        }
+        lds_barrier();
+        if (live) {
+            for (int g = 0; g < G; ++g) {
+                const double v = __longlong_as_double((long long)(((uint64_t)s_fh[4 * g + 1] << 32) | s_fh[4 * g]));
+                const int64_t j = (int64_t)(((uint64_t)s_fh[4 * g + 3] << 32) | s_fh[4 * g + 2]);
+                if (argmin_better(v, j, min_e, p)) { min_e = v; p = j; gw = g; }
+            }
+            const int nw2 = P.pr_stride * 2 - 2;  // 8-byte fields after the entry: KW (+ 2 with Devex)
+            if (wave == 0 && !s_fto) {
+                bool ok = true;
+                for (int k = lane; k < nw2; k += 64) {
+                    uint32_t lo = 0u, hi = 0u;
+                    ok = mbox_poll(P, par, gw, 4 + 2 * k, tag, &lo) && ok;
+                    ok = mbox_poll(P, par, gw, 5 + 2 * k, tag, &hi) && ok;
+                    s_fw[k] = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+                }
+                if (!ok) s_fto = 1;
+            }
+            lds_barrier();
+            if (s_fto) {
+                if (tid == 0) {
+                    st->status = ST_HANDOFF_TIMEOUT;
+                    if (DEFER) P.trec->fresh = 0;
+                }
+                return;
+            }
+        }
     } else {
         for (int g = 0; g < P.nin; ++g) {
             const ArgMinEntry e = P.price_in[g * P.pr_stride];
@@ -2312,7 +2424,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     const bool dvx_grp = P.devex && P.nin > 1;
     double wp_grp = 1.0;
     if (dvx_grp) {
-        const double* ex = dvx_payload(P, gw);
+        const double* ex = P.mbox_fused ? s_fw + KW : dvx_payload(P, gw);
         e_enter = ex[0];
         wp_grp = ex[1];
     }
@@ -2351,8 +2463,9 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     double auv[RPW];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) auv[r] = apd[icl[r]];
-    const double* wrec = P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
-                                   : P.Wt + p * KW;
+    const double* wrec = P.mbox_fused ? s_fw
+                                      : (P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
+                                                   : P.Wt + p * KW);
     const double wlr = wrec[lane < KW ? lane : 0];
     TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (!DEFER && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
@@ -3113,6 +3226,7 @@ __global__ void k_reset(Params P) {
         st->leave = -1;
         st->wp = 1.0;
         st->uncovered = 0u;
+        st->mbox_epoch = st->mbox_epoch + 1u;  // (every rank resets alike)
     }
 }
 
@@ -3692,7 +3806,6 @@ hipError_t launch_cfold(const Params& P, int min_nw, int cus, hipStream_t s) {
 // devices).  A rank that polls for MBOX_TIMEOUT_TICKS without seeing a peer
 // stops with ST_HANDOFF_TIMEOUT, and its later exchanges only send.
 // ---------------------------------------------------------------------------
-constexpr unsigned long long MBOX_TIMEOUT_TICKS = 3000000000ull;  // 30 s of s_memrealtime (100 MHz)
 __global__ __launch_bounds__(256) void k_exchange(Params P) {
     const int tid = threadIdx.x;
     const int G = P.nin;

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_tab_active(Params P, int min_nw) {
 // T_w itself, read and written once; the next block's tiles are loaded after
 // this block's stores (holding them across the MFMAs cost 32 VGPRs and
 // measured slower).  8 waves sharing one U staging, 120 VGPRs, 2 workgroups
-// per CU: 320 -> 260 us at C3 (tools/fold_bench.hip, MALL flushed),
+// per CU: 320 -> 260 us at C3 (round-1 tools/fold_bench.hip, in git history; MALL flushed),
 // bit-identical (the per-element MFMA chain is unchanged).
 // ---------------------------------------------------------------------------
 constexpr int TF_WAVES = 8;
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void k_tab_build(Params P) {
 constexpr int TKW = 64;
 constexpr int TKP = TKW + 1;  // LDS row pitch (doubles): lane-per-row reads hit distinct banks
 #ifndef SPX_TAB_CLK
-// diagnostic stamps of workgroup 0 (tools/tab_clk.sh): clk[0] = pass start,
+// diagnostic stamps of workgroup 0 (round-1 tools/tab_clk.sh, in git history): clk[0] = pass start,
 // clk[2] = barrier 2 done; clk[1] = barrier 1 done (0), or point k of the
 // pass (k = 1 .. 11, TAB_STAMP below) in a build with SPX_TAB_CLK = k
 #define SPX_TAB_CLK 0

@@ -40,13 +40,14 @@ def main():
         st, piv = ctx.iterate(k)
         s = ctx.state(binv=True)
         defer = ctx.config()["defer_tail"]
+        fused = ctx.config()["mbox_fused"]
         if solve:
             r = ctx.solve()
             z, pivots, status = r.z, r.pivots, int(r.status)
         else:
             z, pivots, status = ctx.objective(), piv, int(st)
         np.savez(os.path.join(d, f"r{rank}.npz"), piv=piv, b_ixs=s["b_ixs"], x_b=s["x_b"], y=s["y"],
-                 binv=s["binv"], z=z, pivots=pivots, status=status, defer_tail=defer)
+                 binv=s["binv"], z=z, pivots=pivots, status=status, defer_tail=defer, mbox_fused=fused)
 
 
 if __name__ == "__main__":

@@ -54,7 +54,7 @@ def test_status_strings(spx):
     L = spx._lib.load()
     assert L.spx_status_string(0) == b"MAX_ITER exceeded."
     assert L.spx_status_string(2) == b"Problem unbounded."
-    assert L.spx_abi_version() == 7
+    assert L.spx_abi_version() == 8
 
 
 def _has_gpu():

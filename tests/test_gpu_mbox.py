@@ -20,9 +20,13 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["fused", "k_exchange"])
 @pytest.mark.parametrize("window", [-1, 16])
 @pytest.mark.parametrize("graph_batch", [-1, 16])
-def test_mbox_one_rank_matches_single_rank(spx, window, graph_batch):
+def test_mbox_one_rank_matches_single_rank(spx, monkeypatch, window, graph_batch, fused):
+    """fused: window passes exchange inside k_price / k_ftran_bc (the
+    default); k_exchange: SPX_MBOX_FUSED=0, one exchange kernel per pass."""
+    monkeypatch.setenv("SPX_MBOX_FUSED", fused)
     m, n, seed, k = 300, 1200, 3, 150
     with spx.Context(m=m, n=n, seed=seed, window=window, persist=False) as ref:
         ref.iterate(k)
@@ -35,11 +39,38 @@ def test_mbox_one_rank_matches_single_rank(spx, window, graph_batch):
         s = ctx.state(binv=True)
         p = ctx.price()
     assert piv == k
+    assert cfg["mbox_fused"] == (1 if fused == "1" and window > 0 else 0)
     if graph_batch > 0:  # a plain kernel: the capture never falls back
         assert cfg["graph_batch"] == (16 if window < 0 else 30)
     for key in ("b_ixs", "x_b", "y", "binv"):
         assert np.array_equal(s[key], rs[key]), key
     assert p == rp
+
+
+@pytest.mark.parametrize("graph_batch", [-1, 64])
+def test_mbox_one_rank_fused_deferred_tail(spx, graph_batch):
+    """The fused exchange with the deferred ratio-test tail (m = 2048, compact
+    window passes, 512-thread FTRAN workgroups): k_price's pricing tail stores
+    the record into the mailbox, k_ftran_bc polls it, no k_exchange launch;
+    through two folds the state is the single-rank loop's bit for bit, and so
+    are a reset and a second run (the reset advances the tag epoch, so the
+    first run's words cannot match the second's)."""
+    m, n, seed, k = 2048, 6144, 5, 140
+    with spx.Context(m=m, n=n, seed=seed, window=64, persist=False) as ref:
+        ref.iterate(k)
+        rs = ref.state(binv=True)
+    with spx.Context(m=m, n=n, seed=seed, window=64, comm1=True, graph_batch=graph_batch) as ctx:
+        ctx.mbox_attach([ctx.mbox_export()])
+        cfg = ctx.config()
+        assert cfg["mbox_fused"] == 1 and cfg["defer_tail"] == 1
+        for rep in range(2):
+            if rep:
+                ctx.reset()
+            st, piv = ctx.iterate(k)
+            assert piv == k
+            s = ctx.state(binv=True)
+            for key in ("b_ixs", "x_b", "y", "binv"):
+                assert np.array_equal(s[key], rs[key]), (rep, key)
 
 
 def test_mbox_attach_errors(spx):
@@ -86,6 +117,7 @@ def test_mbox_processes_share_one_gpu(spx, oracle, tmp_path, G, window, graph_ba
         assert int(r["pivots"]) == rr.pivots == o.pivots
         assert float(r["z"]) == rr.z
         assert abs(rr.z - o.z) <= 1e-9 * abs(o.z)
+        assert int(r["mbox_fused"]) == 0  # ranks sharing one GPU keep the k_exchange launch
 
 
 @pytest.mark.parametrize("graph_batch", [16, -1])
@@ -118,6 +150,7 @@ def test_mbox_processes_deferred_tail(spx, tmp_path, graph_batch):
     for g in range(G):
         r = np.load(tmp_path / f"r{g}.npz")
         assert int(r["defer_tail"]) == 1
+        assert int(r["mbox_fused"]) == 0  # (peers on this device: k_exchange, see spx_mbox_attach)
         assert int(r["piv"]) == k
         for key in ("b_ixs", "x_b", "y", "binv"):
             assert np.array_equal(r[key], rs[key]), (g, key)
