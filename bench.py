@@ -152,7 +152,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
     ap.add_argument("--update-rows", type=int, default=0)
     ap.add_argument("--update-block", type=int, default=0)

@@ -36,11 +36,16 @@ EPS = 1e-7
 def _certify(spx, oracle, m, n, seed):
     t0 = time.time()
     with spx.Context(m=m, n=n, seed=seed) as ctx:
-        r = ctx.solve()
+        st, piv = ctx.iterate(0)
+        while st == spx.SolveStatus.MaxIter:  # (in chunks, with a progress line each: the C5 solve takes minutes)
+            st, piv = ctx.iterate(20000)
+            print(f"m={m} n={n}: {piv} pivots after {time.time() - t0:.0f} s", flush=True)
+        r = ctx.solve()  # (terminated: the readback of z, x_B and the basis)
         s = ctx.state()
     t1 = time.time()
-    assert r.status == spx.SolveStatus.OptimumFound
+    assert r.status == spx.SolveStatus.OptimumFound and r.pivots == piv
     A, b, c = oracle.generate(m, n, seed)  # (n, m): row j = column j of A
+    print(f"m={m} n={n}: certificate on the CPU ({time.time() - t1:.0f} s)", flush=True)
     bix = np.asarray(s["b_ixs"], dtype=np.int64)
     x_b = np.asarray(s["x_b"])
     assert len(set(bix.tolist())) == m

@@ -11,7 +11,7 @@ mkdir -p $OUT
 bash tools/gpu_profile.sh $R || exit 1
 P=gpurun_out/prof_$R
 TJ=$P/traffic_$R.json
-timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
 tail -2 $OUT/smoke.log
