@@ -310,8 +310,13 @@ def main():
         t0 = time.perf_counter()
         st, piv1 = ctx.iterate(steps)
         torch.cuda.synchronize()
+        # this rank's span ends at its device sync; the closing barrier only
+        # re-aligns the ranks (with NCCL it is an all-reduce of its own,
+        # 1-3 % of a C3 span when it was inside the clock); the job's time
+        # is the max over ranks of the spans, which all began after one barrier
+        t_end = time.perf_counter()
         barrier()
-        dt = reduce_max([time.perf_counter() - t0])[0]
+        dt = reduce_max([t_end - t0])[0]
         d1 = ctx.dispatch_stats()
         # the averages behind the roofline cover the timed region, not the
         # windows timed after it
@@ -502,6 +507,8 @@ def main():
                                     f"K rounded up to whole captured batches of {cfg['graph_batch']} passes")
                                    + f", at least {MIN_SPAN} pivots (one window's transient does not set the rate)"
                                    if cfg["graph_batch"] > 0 else "none"),
+                "clock": "barrier + device sync, then t0; the K pivots; device sync, then t1 on each rank; "
+                         "barrier; value uses the max over ranks of t1 - t0",
                 "untimed_pivots_before": args.warmup + main_run["lead"],
                 "folds": main_run["dispatch"]["folds"],
                 "graph_launches": main_run["dispatch"]["graph_launches"],
@@ -604,8 +611,9 @@ def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, v
             st, piv = ctx.iterate(4096)
         wd.arm("solve_to_optimum: end", ctx)
         torch.cuda.synchronize()
+        t_end = time.perf_counter()  # (the closing barrier outside the clock, as in timed_window)
         barrier()
-        dt = reduce_max([time.perf_counter() - t0])[0]
+        dt = reduce_max([t_end - t0])[0]
         cols1 = ctx.ftran_cols()
         z = ctx.objective()
         ds = ctx.dispatch_stats()

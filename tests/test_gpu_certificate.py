@@ -23,6 +23,7 @@ the test prints delta * sum(x_B), the bound's value at the solution.
 C4: 35,574 pivots in about 23 s; C5: 137,499 pivots in about 141 s.  Both run
 in the default GPU suite; conftest.py moves them to the end of the run.
 """
+import os
 import time
 
 import numpy as np
@@ -33,19 +34,33 @@ pytestmark = [pytest.mark.gpu, pytest.mark.run_last]
 EPS = 1e-7
 
 
+def _progress(msg):
+    """A progress line on stdout and, on a gpurun box, in gpurun_out/ (the C5
+    solve runs minutes inside one test, with pytest capturing its output)."""
+    print(msg, flush=True)
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root:
+        try:
+            os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+            with open(os.path.join(root, "gpurun_out", "certificate_progress.log"), "a") as f:
+                f.write(msg + "\n")
+        except OSError:
+            pass
+
+
 def _certify(spx, oracle, m, n, seed):
     t0 = time.time()
     with spx.Context(m=m, n=n, seed=seed) as ctx:
         st, piv = ctx.iterate(0)
         while st == spx.SolveStatus.MaxIter:  # (in chunks, with a progress line each: the C5 solve takes minutes)
             st, piv = ctx.iterate(20000)
-            print(f"m={m} n={n}: {piv} pivots after {time.time() - t0:.0f} s", flush=True)
+            _progress(f"m={m} n={n}: {piv} pivots after {time.time() - t0:.0f} s")
         r = ctx.solve()  # (terminated: the readback of z, x_B and the basis)
         s = ctx.state()
     t1 = time.time()
     assert r.status == spx.SolveStatus.OptimumFound and r.pivots == piv
     A, b, c = oracle.generate(m, n, seed)  # (n, m): row j = column j of A
-    print(f"m={m} n={n}: certificate on the CPU ({time.time() - t1:.0f} s)", flush=True)
+    _progress(f"m={m} n={n}: certificate on the CPU ({time.time() - t1:.0f} s)")
     bix = np.asarray(s["b_ixs"], dtype=np.int64)
     x_b = np.asarray(s["x_b"])
     assert len(set(bix.tolist())) == m
