@@ -78,15 +78,6 @@ bool kernels_inplace() { return SPX_INPLACE != 0; }
 #ifndef SPX_BC_PF
 #define SPX_BC_PF 1  // C3 A/B (round-2 tools/r02_abbench.sh, in git history): 1 chunk 12.45k it/s, 2 chunks 12.31-12.34k
 #endif
-#ifndef SPX_PRICE_REC
-// (A/B) deferred pricing passes: k_price's last workgroup
-// (last-arrival count) reduces the partials and publishes one record -- the
-// entering column, its reduced cost, its window coefficients and A_p on the
-// compact column list -- which k_ftran_bc reads at entry instead of reducing
-// the partials and gathering A_p itself.  The record lives in P.rbuf (unused
-// by window passes); compact window passes with S + 68 <= L only.
-#define SPX_PRICE_REC 0
-#endif
 #ifndef SPX_FTRAN_TRIM
 // k_ftran_bc's entry loads: 2 = the U row only up to the window's pending
 // pivots, requested after the state arrives (the default since round 6: PMC
@@ -971,56 +962,6 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         pw[3] = t_pw2;
     }
     if (P.defer_price) {  // k_update reduces the partials after the kernel boundary
-#if SPX_PRICE_REC
-        if constexpr (WIN && WM != 3) {
-            if (tid == 0) {
-                const PricePartial w = red[best_wave<WAVES>(red)];
-                st_agent(&P.price_partials[blockIdx.x].val, w.val);
-                st_agent(&P.price_partials[blockIdx.x].idx, w.idx);
-                st_agent(&P.price_partials[blockIdx.x].w, w.w);
-                st_agent(&P.price_partials[blockIdx.x].pad, w.pad);
-                if (fresh && blockIdx.x == 0) apply_deferred_tail(P, st, s_rec, s_tp);
-                drain_vmem();
-                *s_last = arrive_last(arrive_group(P.arrive, ARR_PRICE), gridDim.x, blockIdx.x);
-            }
-            __syncthreads();
-            if (!*s_last) return;
-            PricePartial w{INFINITY, INT64_MAX, 0.0, 0.0};
-            for (int g = tid; g < (int)gridDim.x; g += BLOCK) {
-                const double v = ld_agent(&P.price_partials[g].val);
-                const int64_t i = ld_agent(&P.price_partials[g].idx);
-                if (argmin_better(v, i, w.val, w.idx))
-                    w = PricePartial{v, i, ld_agent(&P.price_partials[g].w), ld_agent(&P.price_partials[g].pad)};
-            }
-            double bv = w.val;
-            int64_t bj = w.idx;
-            lane_argmin<64>(bv, bj);
-            bv = readlane_d(bv, 63);
-            bj = readlane_l(bj, 63);
-            const uint64_t hit = __ballot(w.val == bv && w.idx == bj);
-            const int wl = hit ? (int)__builtin_ctzll(hit) : 0;
-            const PricePartial o{bv, bj, readlane_d(w.w, wl), readlane_d(w.pad, wl)};
-            __syncthreads();
-            if (lane == 0) red[wave] = o;
-            __syncthreads();
-            PricePartial t = red[0];
-            for (int i = 1; i < WAVES; ++i)
-                if (argmin_better(red[i].val, red[i].idx, t.val, t.idx)) t = red[i];
-            // record: [0] p, [1] min_e, [2] e (Devex), [4..4+64) Wt[p][.], [68..68+S) A_p on the list
-            double* rec = P.rbuf;
-            const bool ok = t.idx != INT64_MAX;
-            if (tid == 0) {
-                reinterpret_cast<int64_t*>(rec)[0] = t.idx;
-                rec[1] = t.val;
-                rec[2] = t.pad;
-            }
-            if (tid < KW) rec[4 + tid] = (!ok || tid >= nw) ? 0.0 : (tid == tau ? t.w : P.Wt[t.idx * KW + tid]);
-            const int Sr = P.bc_n[0];
-            if (ok)
-                for (int c = tid; c < Sr; c += BLOCK) rec[68 + c] = P.A[t.idx * L + P.rlist[c]];
-            return;
-        }
-#endif
         if (tid == 0) {
             P.price_partials[blockIdx.x] = red[best_wave<WAVES>(red)];
             if (fresh && blockIdx.x == 0) {
@@ -2309,14 +2250,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     }
     // ---- entry: everything independent of p (issue order = retire order)
     const int pgi = tid < P.price_grid ? tid : P.price_grid - 1;
-#if SPX_PRICE_REC
-    const double* prec = P.rbuf;  // k_price's record (SPX_PRICE_REC)
-    const int64_t rec_p = reinterpret_cast<const int64_t*>(prec)[0];
-    const double rec_min = prec[1], rec_e = prec[2];
-    const PricePartial pwl{rec_min, rec_p, 0.0, rec_e};
-#else
     const PricePartial pwl = P.price_partials[pgi];
-#endif
     int32_t rlv[BC_RL];
 #pragma unroll
     for (int j = 0; j < BC_RL; ++j) {
@@ -2390,13 +2324,6 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     __shared__ uint32_t s_fh[4 * MBOX_FUSED_MAX_G];
     __shared__ double s_fw[64 + 2];
     __shared__ int s_fto;
-#if SPX_PRICE_REC
-    if (P.defer_price) {
-        min_e = pwl.val;
-        p = pwl.idx;
-        e_enter = pwl.pad;
-    } else
-#endif
     if (P.defer_price) {
         PricePartial w = tid < P.price_grid ? pwl : PricePartial{INFINITY, INT64_MAX, 0.0, 0.0};
         for (int g = tid + BLOCK; g < P.price_grid; g += BLOCK) {
@@ -2531,12 +2458,6 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     // slots past S would multiply the L2 requests for nothing)
     const double* apd = P.A + p * P.L;
     double apv[BC_RL];
-#if SPX_PRICE_REC
-    if (P.defer_price) {
-#pragma unroll
-        for (int j = 0; j < BC_RL; ++j) apv[j] = (tid + j * BLOCK < Sbc) ? prec[68 + tid + j * BLOCK] : 0.0;
-    } else
-#endif
 #pragma unroll
     for (int j = 0; j < BC_RL; ++j) apv[j] = (tid + j * BLOCK < Sbc) ? apd[rlv[j]] : 0.0;
     double auv[RPW];
@@ -2544,11 +2465,7 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
     for (int r = 0; r < RPW; ++r) auv[r] = apd[icl[r]];
     const double* wrec = P.mbox_fused ? s_fw
                                       : (P.nin > 1 ? reinterpret_cast<const double*>(P.price_in + gw * P.pr_stride + 1)
-#if SPX_PRICE_REC
-                                                   : (P.defer_price ? prec + 4 : P.Wt + p * KW));
-#else
                                                    : P.Wt + p * KW);
-#endif
     const double wlr = wrec[lane < KW ? lane : 0];
     TailPre tpre{0, 0.0, 0, -1, -1, 0.0, 0, 0.0, 0};
     if (!DEFER && tid == 0 && !P.split_tail) tpre = tail_prefetch(P, Sv.nw, Sv.nb_count, p);
