@@ -8,7 +8,8 @@ only; the GPU tests solve C4 to optimality and compare with it
 
     python tests/golden/make_golden_c4.py [m n seed]
     (committed: 4096 65536 0 -> highs_4096x65536_0.json; 16384 20480 0 ->
-    highs_16384x20480_0.json, C5's height, tests/test_gpu_c5_optimum.py)
+    highs_16384x20480_0.json, C5's height, tests/test_gpu_c5_optimum.py;
+    8192 24576 0 -> highs_8192x24576_0.json, tests/test_gpu_m8192_optimum.py)
 
 The basis is read from x as make_golden.highs_optimum does (the m largest
 entries); the LP is the same as there.
