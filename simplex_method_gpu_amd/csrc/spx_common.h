@@ -44,6 +44,14 @@ __device__ __forceinline__ dbl2 ld2(const dbl2* p) {
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
+// A raw buffer load of 16 bytes at byte offset off of the range rs: lanes past
+// the range's size read 0 and send no memory request (word 3 of a gfx9 raw
+// buffer resource: 32-bit data format, no swizzle; aux 2 = nt)
+#define SPX_BUF_DW3 0x00020000
+template <int NT>
+__device__ __forceinline__ dbl2 ldbuf2(__amdgpu_buffer_rsrc_t rs, int off) {
+    return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, NT ? 2 : 0));
+}
 template <int NT>
 __device__ __forceinline__ void st2(dbl2 v, dbl2* p) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);

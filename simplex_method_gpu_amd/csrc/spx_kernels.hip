@@ -53,11 +53,19 @@ namespace spx {
 #ifndef SPX_PRICE_DEEP
 #define SPX_PRICE_DEEP 1  // deferred tail: the first column's first 16 chunks requested before the reduction
 #endif
+#ifndef SPX_SE_LDS_BATCH
+// steepest edge (WM 4): its LDS operand batch (0 = SPX_LDS_BATCH); 2 frees
+// the registers its two-batch deep prefetch needs (248 VGPRs, no spills)
+#define SPX_SE_LDS_BATCH 2
+#endif
 #ifndef SPX_PRICE_DEEP1
 #define SPX_PRICE_DEEP1 0  // (A/B, with SPX_PRICE_DEEP=0) WM 1 with the one-batch deep prefetch
 #endif
 #ifndef SPX_PRICE_DEEP_SE
-#define SPX_PRICE_DEEP_SE 0  // steepest edge (WM 4): the first column's first 8 chunks requested before it
+// steepest edge (WM 4): the first column's first 8 (1) or 16 (2, the default
+// since round 6: k_price 0.711 -> 0.725 of 8 TB/s, profiles/r06_steepest_ab.txt)
+// chunks requested before the deferred-tail reduction
+#define SPX_PRICE_DEEP_SE 2
 #endif
 #ifndef SPX_PRICE_DYN_PCT
 #define SPX_PRICE_DYN_PCT 85  // the share of the columns handed out statically (grid stride)
@@ -286,6 +294,7 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     int32_t pk_a = -1, pk_b = -1;
     int64_t pv_a = 0, pv_b = 0;
     constexpr int CH = (BLOCK <= 512 && WM != 3) ? SPX_PRICE_CH : 8;
+    constexpr int LB = (WM == 4 && SPX_SE_LDS_BATCH > 0) ? SPX_SE_LDS_BATCH : SPX_LDS_BATCH;  // LDS operand batch
     // SPX_PRICE_DEEP (deferred tail): the first column's first 2 CH chunks are
     // requested as soon as the tail's record says which column this slot
     // holds after the pivot's list edit -- before the partials are reduced
@@ -297,7 +306,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // (only run_pipe consumes vd0 / vd1, so DEEP needs the pipelined loop)
     // (steepest edge, WM 4: its third dot leaves room for the first batch only,
     // SPX_PRICE_DEEP_SE; two batches spilled)
-    constexpr bool DEEP2 = SPX_PRICE_DEEP && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8;
+    constexpr bool DEEP2 = SPX_PRICE_DEEP && SPX_PRICE_PIPE && BLOCK <= 512 && CH == 8 &&
+                           (WM == 1 || (SPX_PRICE_DEEP_SE == 2 && WM == 4));
     constexpr bool DEEP = DEEP2 || (SPX_PRICE_DEEP_SE && SPX_PRICE_PIPE && WM == 4 && BLOCK <= 512 && CH == 8) ||
                           (SPX_PRICE_DEEP1 && SPX_PRICE_PIPE && WM == 1 && BLOCK <= 512 && CH == 8);
     dbl2 vd0[DEEP ? CH : 1], vd1[DEEP2 ? CH : 1];
@@ -312,26 +322,28 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
         if constexpr (DEEP) {
             // slots below cnt0 hold the same column before and after the
             // list edit, except p's slot R.kp, which takes the last entry.
-            // The loads are unconditional (column and chunk clamped): behind
-            // a branch, the compiler's waits for the partials below covered
-            // these 16 loads too (the wait counts of the two paths merge)
+            // The loads are unconditional buffer loads: behind a branch, the
+            // compiler's waits for the partials below covered these loads too
+            // (the wait counts of the two paths merge).  Their range is the
+            // prefetched chunks when the record is fresh and the slot prices
+            // a column, else 0 bytes: out-of-range lanes read 0 and send no
+            // request, so a pass after the optimum (the rest of an iterate()
+            // call; it prices nothing) no longer streams 16-32 KB per wave
             const int64_t L2d = P.L >> 1;
-            const int32_t cnt0 = fresh ? (R.kp >= 0 ? R.cnt - 1 : R.cnt) : S.nb_count;
-            const bool dv = idx0 < cnt0 && (L2d & 511) == 0 && L2d >= 2 * CH * 64;
-            int64_t jd = (fresh && R.kp >= 0 && idx0 == R.kp) ? (int64_t)R.last : j0;
+            const int32_t cnt0 = R.kp >= 0 ? R.cnt - 1 : R.cnt;
+            const bool dv = fresh && idx0 < cnt0 && (L2d & 511) == 0 && L2d >= 2 * CH * 64;
+            int64_t jd = (R.kp >= 0 && idx0 == R.kp) ? (int64_t)R.last : j0;
             jd = (uint64_t)jd < (uint64_t)P.n ? jd : 0;
-            const dbl2* cd = reinterpret_cast<const dbl2*>(P.A + jd * P.L);
+            constexpr int NB = (DEEP2 ? 2 : 1) * CH * 64 * (int)sizeof(dbl2);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double*>(P.A + jd * P.L), 0, dv ? NB : 0, SPX_BUF_DW3);
 #pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int64_t k = lane + u * 64;
-                vd0[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
-            }
+            for (int u = 0; u < CH; ++u)
+                vd0[u] = ldbuf2<SPX_NT_A>(rs, (lane + u * 64) * (int)sizeof(dbl2));
             if constexpr (DEEP2) {
 #pragma unroll
-                for (int u = 0; u < CH; ++u) {
-                    const int64_t k = CH * 64 + lane + u * 64;
-                    vd1[u] = ld2<SPX_NT_A>(&cd[k < L2d ? k : L2d - 1]);
-                }
+                for (int u = 0; u < CH; ++u)
+                    vd1[u] = ldbuf2<SPX_NT_A>(rs, (CH * 64 + lane + u * 64) * (int)sizeof(dbl2));
             }
             jdeep = dv ? jd : -1;
         }
@@ -725,17 +737,17 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
             constexpr bool PD = decltype(pend_t)::value;
             auto consume = [&](const dbl2* vv, int nb8, int64_t kb) {
 #pragma unroll
-                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
+                for (int h = 0; h < 8; h += LB) {
                     if (h >= nb8) break;
-                    dbl2 w[SPX_LDS_BATCH], r[SPX_LDS_BATCH], x[SPX_LDS_BATCH];
+                    dbl2 w[LB], r[LB], x[LB];
 #pragma unroll
-                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                    for (int u = 0; u < LB; ++u) {
                         w[u] = Y(kb + lane + (h + u) * 64);
                         if constexpr (PD) r[u] = Rw(kb + lane + (h + u) * 64);
                         if constexpr (PD && SE) x[u] = Vw(kb + lane + (h + u) * 64);
                     }
 #pragma unroll
-                    for (int u = 0; u < SPX_LDS_BATCH; ++u) {
+                    for (int u = 0; u < LB; ++u) {
                         a0 = fma(vv[h + u].x, w[u].x, a0);
                         a1 = fma(vv[h + u].y, w[u].y, a1);
                         if constexpr (PD) {
@@ -856,18 +868,18 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
                 dbl2 v[8], w[8], r[8], x[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[u] = ld2<SPX_NT_A>(&col[k + u * 64]);
-                // LDS operands fetched SPX_LDS_BATCH elements at a time (one
+                // LDS operands fetched LB elements at a time (one
                 // LDS latency per batch, not one per element)
 #pragma unroll
-                for (int h = 0; h < 8; h += SPX_LDS_BATCH) {
+                for (int h = 0; h < 8; h += LB) {
 #pragma unroll
-                    for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
+                    for (int u = h; u < h + LB; ++u) {
                         w[u] = Y(k + u * 64);
                         r[u] = Rw(k + u * 64);
                         if constexpr (SE) x[u] = Vw(k + u * 64);
                     }
 #pragma unroll
-                    for (int u = h; u < h + SPX_LDS_BATCH; ++u) {
+                    for (int u = h; u < h + LB; ++u) {
                         a0 = fma(v[u].x, w[u].x, a0);
                         a1 = fma(v[u].y, w[u].y, a1);
                         b0 = fma(v[u].x, r[u].x, b0);
