@@ -63,8 +63,8 @@ namespace spx {
 #endif
 #ifndef SPX_PRICE_DEEP_SE
 // steepest edge (WM 4): the first column's first 8 (1) or 16 (2, the default
-// since round 6: k_price 0.711 -> 0.725 of 8 TB/s, profiles/r06_steepest_ab.txt)
-// chunks requested before the deferred-tail reduction
+// since round 6: k_price 0.711 -> 0.721 of 8 TB/s, pass 87.9 -> 86.4 us,
+// profiles/r06_steepest_ab.txt) chunks requested before the deferred-tail reduction
 #define SPX_PRICE_DEEP_SE 2
 #endif
 #ifndef SPX_PRICE_DYN_PCT
@@ -304,8 +304,8 @@ __global__ __launch_bounds__(BLOCK) void k_price(Params P) {
     // shape): with the base row read from L2 (WM 2, C5) it measured 4.6 %
     // slower per pass (1,071 against 1,022 us, tools/pass_ab.py).
     // (only run_pipe consumes vd0 / vd1, so DEEP needs the pipelined loop)
-    // (steepest edge, WM 4: its third dot leaves room for the first batch only,
-    // SPX_PRICE_DEEP_SE; two batches spilled)
+    // (steepest edge, WM 4: both batches with its LDS operand batch at 2,
+    // SPX_SE_LDS_BATCH; at the default batch the second one spilled)
     constexpr bool DEEP2 = SPX_PRICE_DEEP && SPX_PRICE_PIPE && BLOCK <= 512 && CH == 8 &&
                            (WM == 1 || (SPX_PRICE_DEEP_SE == 2 && WM == 4));
     constexpr bool DEEP = DEEP2 || (SPX_PRICE_DEEP_SE && SPX_PRICE_PIPE && WM == 4 && BLOCK <= 512 && CH == 8) ||
