@@ -589,12 +589,42 @@ def main():
         dist.destroy_process_group()
 
 
+SOLVE_CHUNKS = "16, 32, ..., 2048, then 2048 per call"
+
+
+def run_to_exit(ctx, arm=None):
+    """Iterate from the current basis until the solve terminates, in
+    spx_solve's chunks (spx_api.cpp, `spx_solve`: 16 pivots, doubling to 2,048
+    per spx_iterate call; the status is read back after each call). A call
+    enqueues all its passes, so the passes after the optimum inside the last
+    call price nothing (the larger the chunk, the more of them).
+    Returns (status, pivots, calls)."""
+    st, piv = ctx.iterate(0)
+    chunk, calls = 16, 0
+    while st == 0:  # SolveStatus.MaxIter: not terminated yet
+        if arm is not None:
+            arm(chunk, piv)  # one call's bound
+        st, piv = ctx.iterate(chunk)
+        calls += 1
+        chunk = min(2 * chunk, 2048)
+    return st, piv, calls
+
+
+def calls_passes(calls):
+    """Passes enqueued by `calls` spx_iterate calls of run_to_exit's schedule."""
+    tot, chunk = 0, 16
+    for _ in range(calls):
+        tot += chunk
+        chunk = min(2 * chunk, 2048)
+    return tot
+
+
 def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, value, wd):
     """The whole solve of the headline LP: the default path from the slack
     basis to optimality on the same clock as `value` (barrier + device sync on
     both sides, max over ranks), dispatched as the library does it (captured
     hipGraphs of whole windows plus a few eager passes at the ends of each
-    spx_iterate call).  `value` samples an early window, where the compact
+    spx_iterate call; spx_solve's chunk schedule, `run_to_exit`).  `value` samples an early window, where the compact
     FTRAN operand is narrow (S columns of B_w that are not unit); S grows over
     the solve, and so does the FTRAN pass."""
     with wd.phase("solve_to_optimum: context"):
@@ -605,10 +635,7 @@ def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, v
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        st, piv = ctx.iterate(0)
-        while st == 0:  # SolveStatus.MaxIter: not terminated yet
-            wd.arm(f"solve_to_optimum: iterate(4096) from pivot {piv}", ctx)  # one call's bound
-            st, piv = ctx.iterate(4096)
+        st, piv, calls = run_to_exit(ctx, lambda k, p: wd.arm(f"solve_to_optimum: iterate({k}) from pivot {p}", ctx))
         wd.arm("solve_to_optimum: end", ctx)
         torch.cuda.synchronize()
         t_end = time.perf_counter()  # (the closing barrier outside the clock, as in timed_window)
@@ -626,7 +653,8 @@ def solve_to_optimum_block(make, barrier, reduce_max, torch, window, main_run, v
             "ftran_cols_start": cols0, "ftran_cols_end": cols1,
             "vs_value": rate / value if value > 0 else None,
             "dispatch": f"{ds['graph_launches']} hipGraph replays ({ds['graph_passes']} passes) + "
-                        f"{ds['eager_passes']} eager passes; {ds['folds']} folds",
+                        f"{ds['eager_passes']} eager passes; {ds['folds']} folds; {calls} spx_iterate calls "
+                        f"({SOLVE_CHUNKS}), {calls_passes(calls) - piv} passes after the optimum",
             "note": "time to optimum from the slack basis (the v4:286-359 loop run to its exit, as the "
                     "reference CLI times it at v4:456-471); `value` times one early window "
                     f"(ftran_cols {main_run['ftran_cols']} there)"}
@@ -671,9 +699,7 @@ def steepest_block(spx, torch, m, n, args, device):
     with ctx_() as ctx:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        st, tot = ctx.iterate(0)
-        while st == 0:
-            st, tot = ctx.iterate(4096)
+        st, tot, calls = run_to_exit(ctx)
         torch.cuda.synchronize()
         sdt = time.perf_counter() - t0
         z = ctx.objective()
@@ -684,7 +710,8 @@ def steepest_block(spx, torch, m, n, args, device):
             "k_update_ms": pt["update_ms"] / passes,
             "event_timed_ms_per_step": 1e3 * dt_e / max(piv_e, 1),
             "solve": {"status": ["MaxIter", "OptimumFound", "Unbounded", "ThetaOverflow"][int(st)],
-                      "pivots": int(tot), "seconds": sdt, "z": z},
+                      "pivots": int(tot), "seconds": sdt, "z": z, "iterate_calls": calls,
+                      "passes_after_optimum": calls_passes(calls) - int(tot)},
             "representation": f"eta window {cfg['window']}, two-kernel passes; k_price carries a third "
                               "dot on the A stream (B_w^T alpha beside y_w and the base row)"}
 
