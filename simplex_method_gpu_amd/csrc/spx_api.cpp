@@ -116,6 +116,12 @@ struct spx_ctx {
     bool slack_ident = false;  // A[:, n-m:] = I (checked before setup_common)
     bool defer_ok = false;        // loop passes defer the pricing tail into k_update (Params::defer_price)
     bool defer_tail = false;      // loop passes defer the ratio-test tail into k_price (Params::defer_tail)
+    // steepest edge: k_ftran_bc stores k_se_part's sums (Params::se_fused) when
+    // se_fuse is set; se_chain = the last pass enqueued did, and nothing since
+    // changed B_w, U or alpha, so the next pass's k_se_fin reads them
+    bool se_fuse = false;
+    bool se_chain = false;
+    int64_t se_rows = 0;
 
     // graph replay of `batch` passes
     hipGraphExec_t graph_exec = nullptr;
@@ -366,9 +372,11 @@ int setup_common(spx_ctx* x, int64_t m, int64_t n, const spx_opts* opts) {
     P.win = KW > 0 ? KW : 0;
     if (P.steep) {  // B_w^T alpha (L), U^T alpha + gamma_p (KW + 1), row-block partials
         P.se_parts = se_parts_for(m);
+        // rows: k_se_part's blocks, or one per k_ftran_bc workgroup (8 rows each, se_fused)
+        x->se_rows = std::max<int64_t>(P.se_parts, (m + 7) / 8);
         SPX_TRY(x->alloc(&P.se_v, (size_t)L));
         SPX_TRY(x->alloc(&P.se_cg, (size_t)(KW + 1)));
-        SPX_TRY(x->alloc(&P.se_part, (size_t)P.se_parts * (size_t)(L + KW + 1)));
+        SPX_TRY(x->alloc(&P.se_part, (size_t)x->se_rows * (size_t)(L + KW + 1)));
     }
     if (P.win) {
         SPX_TRY(x->alloc(&P.U, (size_t)(m * KW)));
@@ -713,8 +721,11 @@ int enqueue_pass(spx_ctx* x, bool timed) {
         if (f1) HIP_TRY(hipEventRecord(f1, x->stream));
     }
     advance_window(x, fold);
-    HIP_TRY(launch_se_prep(x->P, x->stream));  // steepest edge: after the fold, before pricing
+    // steepest edge: after the fold, before pricing (k_se_part skipped when the
+    // previous pass's FTRAN left its sums and no fold came between)
+    HIP_TRY(launch_se_prep(x->P, x->stream, (x->se_fuse && x->se_chain && !fold) ? x->ucfg.grid : 0));
     Params Pp = x->P;  // loop passes: the pricing tail is reduced by k_update
+    Pp.se_fused = x->se_fuse ? 1 : 0;
     Pp.defer_price = x->defer_ok ? 1 : 0;
     Pp.defer_tail = x->defer_tail ? 1 : 0;
     Pp.mbox_fused = (x->mbox_ready && x->mbox_fused) ? 1 : 0;
@@ -730,6 +741,7 @@ int enqueue_pass(spx_ctx* x, bool timed) {
     }
     if (timed) HIP_TRY(hipEventRecord(x->ev_xend[x->n_price - 1], x->stream));
     HIP_TRY(launch_update(Pp, x->ucfg, x->stream, u0, u1));
+    x->se_chain = x->se_fuse;
     if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
     if (x->P.row_shard) {  // ratio-test all-gather (header + candidate row), then finalise
         if (!x->comm_ready) return fail(SPX_ERR_STATE, "row-sharded B^-1 needs spx_attach_comm");
@@ -751,6 +763,7 @@ int build_graph(spx_ctx* x) {
     x->graph_folds = 0;
     for (int i = 0; i < x->batch && rc == SPX_OK; ++i) rc = enqueue_pass(x, false);
     x->capturing = false;
+    x->se_chain = false;  // (nothing captured has run)
     x->nw = nw_keep;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(x->stream, &g);
@@ -955,6 +968,7 @@ int iterate_raw(spx_ctx* x, int64_t k) {
     }
     if (x->stepped_price) return fail(SPX_ERR_STATE, "spx_price was called without spx_pivot");
     SPX_TRY(set_limit(x, x->pivots + k));
+    x->se_chain = false;  // (steepest edge: the fused sums are used within one call only)
     // exactly k passes: whole captured batches, then the remainder eagerly.
     // Eta window: batches are captured starting with a fold, so eager passes
     // first bring the window to nw == KW.
@@ -967,6 +981,7 @@ int iterate_raw(spx_ctx* x, int64_t k) {
             SPX_TRY(build_graph(x));
             const int64_t reps = left / x->batch;
             for (int64_t i = 0; i < reps; ++i) HIP_TRY(hipGraphLaunch(x->graph_exec, x->stream));
+            x->se_chain = false;
             x->n_graph_launch += reps;
             x->n_graph_pass += reps * x->batch;
             x->n_folds += reps * x->graph_folds;
@@ -975,6 +990,7 @@ int iterate_raw(spx_ctx* x, int64_t k) {
     }
     for (int64_t i = 0; i < left; ++i) SPX_TRY(enqueue_pass(x, x->timing));
     if (x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));  // the last pass's tail, before any readback
+    x->se_chain = false;
     return read_state(x);
 }
 
@@ -1174,6 +1190,8 @@ int set_slack_flags(spx_ctx* x) {
         x->P.tail_parts = uc.grid;
         x->defer_tail = true;
     }
+    // (measured: tools/r6_sefuse.sh; SPX_SE_FUSE=0 keeps k_se_part)
+    x->se_fuse = x->P.steep && x->defer_tail && uc.bc_entry == 1 && uc.grid <= x->se_rows && !env_off("SPX_SE_FUSE");
     return SPX_OK;
 }
 
@@ -1466,6 +1484,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
         for (int g = 0; g < G; ++g) {
             HIP_TRY(hipSetDevice(cs[g]->device));
             SPX_TRY(set_limit(cs[g], cs[g]->pivots + k));
+            cs[g]->se_chain = false;
         }
         for (int64_t it = 0; it < k; ++it) {
             for (int g = 0; g < G; ++g) {  // pricing on every shard
@@ -1475,7 +1494,8 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 if (fold && x->defer_tail) HIP_TRY(launch_apply_tail(x->P, x->stream));
                 if (fold) HIP_TRY(launch_fold(x->P, x->P.win, x->cus, x->stream));
                 advance_window(x, fold);
-                HIP_TRY(launch_se_prep(x->P, x->stream));  // steepest edge: after the fold, before pricing
+                // steepest edge: after the fold, before pricing (as enqueue_pass)
+                HIP_TRY(launch_se_prep(x->P, x->stream, (x->se_fuse && x->se_chain && !fold) ? x->ucfg.grid : 0));
                 ++x->n_eager;
                 x->n_folds += fold ? 1 : 0;
                 Params Pp = x->P;  // the deferred ratio-test tail (each rank's own FTRAN partials)
@@ -1500,7 +1520,9 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
                 HIP_TRY(hipSetDevice(x->device));
                 Params Pp = x->P;
                 Pp.defer_tail = x->defer_tail ? 1 : 0;
+                Pp.se_fused = x->se_fuse ? 1 : 0;
                 HIP_TRY(launch_update(Pp, x->ucfg, x->stream, nullptr, nullptr));
+                x->se_chain = x->se_fuse;
                 if (x->P.split_tail) HIP_TRY(launch_tail(x->P, x->ucfg.grid, x->stream));
                 if (rs) HIP_TRY(hipEventRecord(x->ev_sent2, x->stream));
                 else
@@ -1531,6 +1553,7 @@ int spx_group_iterate(spx_ctx** cs, int32_t G, int64_t k, int32_t* status, int64
         for (int g = 0; g < G; ++g) {
             HIP_TRY(hipSetDevice(cs[g]->device));
             if (cs[g]->defer_tail) HIP_TRY(launch_apply_tail(cs[g]->P, cs[g]->stream));  // the last pass's tail
+            cs[g]->se_chain = false;
             SPX_TRY(read_state(cs[g]));
         }
         for (int g = 1; g < G; ++g)

@@ -339,7 +339,10 @@ struct Params {
     double* bc;
     double* bc1;
     int32_t cfold;  // the fold updates the listed columns only (k_cfold; SPX_DENSE_FOLD=1: k_fold + gather)
-    int32_t pad_bc;
+    // steepest edge, set per launch: k_ftran_bc stores its workgroup's
+    // partial sums of M^T alpha (k_se_part's, over its 8 rows) into se_part,
+    // so the next pass's k_se_fin can skip k_se_part (spx_api.cpp se_chain)
+    int32_t se_fused;
     int32_t* rlist;
     int32_t* rmap;
     int32_t* rleft;

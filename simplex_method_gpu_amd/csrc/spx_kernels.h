@@ -46,7 +46,7 @@ hipError_t launch_fold(const Params& P, int min_nw, int cus, hipStream_t s);
 // steepest edge (P.steep): weights at the slack basis; B_w^T alpha, U^T alpha
 // and gamma_p of the pending pivot before a pricing pass
 hipError_t launch_se_init(const Params& P, hipStream_t s);
-hipError_t launch_se_prep(const Params& P, hipStream_t s);
+hipError_t launch_se_prep(const Params& P, hipStream_t s, int fused_parts = 0);  // fused_parts: the FTRAN pass's partials
 int se_parts_for(int64_t m);
 
 }  // namespace spx

@@ -2238,7 +2238,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(Params P) {
 // partials' reduction, A_p's gather on the list) is done by RPW times fewer
 // workgroups, each wave keeps RPW rows' loads in flight, and the grid fits
 // one workgroup per CU (<= 256 VGPRs).
-template <int BLOCK, bool DEFER, int RPW>
+// SEF (steepest edge, Params::se_fused): its own instantiation, so the
+// Dantzig / Devex pass keeps its code
+template <int BLOCK, bool DEFER, int RPW, bool SEF = false>
 __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) {
     static_assert(RPW == 1 || DEFER, "several rows per wave: the deferred-tail form only");
     DevState* st = P.st;
@@ -2670,6 +2672,40 @@ __global__ __launch_bounds__(BLOCK, RPW == 1 ? 4 : 2) void k_ftran_bc(Params P) 
                 rec->last = rlast;
                 rec->nw = Sv.nw;
                 rec->fresh = 1;
+            }
+        }
+        if constexpr (SEF && RPW == 1) {
+            {
+                // steepest edge, k_se_part's sums fused (the pending pivot is
+                // this pass's: alpha = al, U[i][s] for s <= tau = cu): this
+                // workgroup's rows' terms of M^T alpha for M = [B_w at the S
+                // listed columns | U[:, s < nw] | alpha], summed over its waves
+                // in row order, in LDS blocks of sec columns (the A_p list's
+                // space: every wave has passed its last read of it)
+                const int64_t Ls = P.L;
+                const int ncol = S + KW + 1;
+                const int sec = (int)((Ls < BC_APC ? Ls : BC_APC) / WAVES);
+                const double av = rowv[0] ? al[0] : 0.0;
+                const double cuv = rowv[0] ? (lane < tau ? urow[0] : (lane == tau ? ei[0] : 0.0)) : 0.0;
+                const double* rowp = bcb + icl[0] * ldc;
+                double* outp = P.se_part + (int64_t)blockIdx.x * (Ls + KW + 1);
+                double* sp = apc + wave * sec;
+                for (int c0 = 0; c0 < ncol; c0 += sec) {
+                    const int c1 = ncol < c0 + sec ? ncol : c0 + sec;
+                    if (c0 > 0) lds_barrier();  // the previous block's sums are read
+                    for (int c = c0 + lane; c < c1; c += 64) {
+                        if (c < S) sp[c - c0] = rowp[c] * av;
+                        else if (c == S + KW) sp[c - c0] = av * av;
+                    }
+                    if (lane < KW && S + lane >= c0 && S + lane < c1) sp[S + lane - c0] = cuv * av;
+                    lds_barrier();
+                    for (int c = c0 + tid; c < c1; c += BLOCK) {
+                        double t = apc[c - c0];
+#pragma unroll
+                        for (int w = 1; w < WAVES; ++w) t += apc[w * sec + c - c0];
+                        outp[c] = t;
+                    }
+                }
             }
         }
         store_row();
@@ -3345,20 +3381,20 @@ static hipError_t launch_update_k(const Params& P, int grid, hipStream_t s, hipE
 
 // grid: the one-row grid's workgroups (= partial slots); RPW rows per wave
 // take ceil(grid / RPW) workgroups
-template <int BLOCK, bool DEFER, int RPW>
+template <int BLOCK, bool DEFER, int RPW, bool SEF = false>
 static hipError_t launch_ftran_bc_t(const Params& P, int grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const size_t red = RPW == 1 ? UpdLds<BLOCK>::bytes : sizeof(UpdPartial) * (BLOCK / 64) * RPW + 16;
     const size_t lds = red + (size_t)(P.L < BC_APC ? P.L : BC_APC) * 8;
     const int g = (grid + RPW - 1) / RPW;
     if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK, DEFER, RPW>),
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ftran_bc<BLOCK, DEFER, RPW, SEF>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024);
         if (e != hipSuccess) return e;
     }
     if (e0 || e1)
-        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW>), dim3(g), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
+        hipExtLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW, SEF>), dim3(g), dim3(BLOCK), (uint32_t)lds, s, e0, e1, 0, P);
     else
-        hipLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW>), dim3(g), dim3(BLOCK), lds, s, P);
+        hipLaunchKernelGGL((k_ftran_bc<BLOCK, DEFER, RPW, SEF>), dim3(g), dim3(BLOCK), lds, s, P);
     return hipGetLastError();
 }
 
@@ -3371,6 +3407,7 @@ static hipError_t launch_ftran_bc(const Params& P, int grid, int rpw, hipStream_
     if constexpr (BLOCK == 512) {
         if (rpw == 2) return launch_ftran_bc_t<BLOCK, true, 2>(P, grid, s, e0, e1);
         if (rpw == 4) return launch_ftran_bc_t<BLOCK, true, 4>(P, grid, s, e0, e1);
+        if (P.se_fused) return launch_ftran_bc_t<BLOCK, true, 1, true>(P, grid, s, e0, e1);
     }
     return launch_ftran_bc_t<BLOCK, true, 1>(P, grid, s, e0, e1);
 }
@@ -4071,11 +4108,16 @@ hipError_t launch_se_init(const Params& P, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_se_prep(const Params& P, hipStream_t s) {
+hipError_t launch_se_prep(const Params& P, hipStream_t s, int fused_parts) {
     if (!P.steep) return hipSuccess;
-    hipLaunchKernelGGL(k_se_part, dim3((unsigned)P.se_parts), dim3(256), 0, s, P);
+    Params Q = P;
+    if (fused_parts > 0) {
+        Q.se_parts = fused_parts;  // the previous k_ftran_bc's workgroup partials (Params::se_fused)
+    } else {
+        hipLaunchKernelGGL(k_se_part, dim3((unsigned)P.se_parts), dim3(256), 0, s, P);
+    }
     // 64 columns per workgroup (the columns in use, S + KW + 1, are at most L + KW + 1)
-    hipLaunchKernelGGL(k_se_fin, dim3((unsigned)((P.L + P.win + 1 + 63) / 64)), dim3(1024), 0, s, P);
+    hipLaunchKernelGGL(k_se_fin, dim3((unsigned)((P.L + P.win + 1 + 63) / 64)), dim3(1024), 0, s, Q);
     return hipGetLastError();
 }
 

@@ -178,3 +178,28 @@ def test_steepest_c3_solves_to_highs_optimum(spx):
     assert abs(r.z - h["highs_z"]) <= 1e-9 * abs(h["highs_z"])
     assert sorted(int(j) for j in r.b_ixs) == h["highs_basis"]
     assert r.pivots < h["oracle_pivots"]
+
+
+@pytest.mark.parametrize("m,n,k", [(2048, 8192, 300), (4096, 16384, 200)])
+def test_steepest_fused_partials_match_k_se_part(spx, m, n, k):
+    """k_ftran_bc's fused sums of M^T alpha (Params::se_fused; k_se_part
+    skipped on every pass but the first after a fold) against k_se_part's
+    (SPX_SE_FUSE=0): the same pivots, and weights, x_b and y within 1e-12
+    (relative) -- the two group the same terms differently (8-row workgroups
+    against 16-row blocks), so the bits may differ."""
+    out = {}
+    for fuse in ("1", "0"):
+        with _env(SPX_SE_FUSE=fuse):
+            with spx.Context(m=m, n=n, seed=1, pricing=STEEP, trace=k) as ctx:
+                st, piv = ctx.iterate(k)
+                tp, tq = ctx.trace()
+                s = ctx.state()
+                out[fuse] = (st, piv, tp, tq, s["x_b"], s["y"], ctx.weights(), s["b_ixs"])
+    a, b = out["1"], out["0"]
+    assert a[:2] == b[:2]
+    assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+    assert np.array_equal(a[7], b[7])
+    for i in (4, 5):
+        assert np.max(np.abs(a[i] - b[i])) <= 1e-12 * max(1.0, float(np.max(np.abs(b[i]))))
+    nb = _nonbasic(n, a[7])
+    assert np.max(np.abs(a[6][nb] - b[6][nb]) / b[6][nb]) <= 1e-12
