@@ -184,9 +184,11 @@ def test_steepest_c3_solves_to_highs_optimum(spx):
 def test_steepest_fused_partials_match_k_se_part(spx, m, n, k):
     """k_ftran_bc's fused sums of M^T alpha (Params::se_fused; k_se_part
     skipped on every pass but the first after a fold) against k_se_part's
-    (SPX_SE_FUSE=0): the same pivots, and weights, x_b and y within 1e-12
-    (relative) -- the two group the same terms differently (8-row workgroups
-    against 16-row blocks), so the bits may differ."""
+    (SPX_SE_FUSE=0): the same pivots, x_b and y within 1e-12 and the weights
+    within 1e-9 (relative; the oracle test's bound) -- the two group the same
+    terms differently (8-row workgroups against 16-row blocks), so the bits
+    differ, and the Goldfarb-Reid recurrence carries that rounding from pass
+    to pass (measured: 1.8e-11 after 300 pivots at m = 2048)."""
     out = {}
     for fuse in ("1", "0"):
         with _env(SPX_SE_FUSE=fuse):
@@ -202,4 +204,4 @@ def test_steepest_fused_partials_match_k_se_part(spx, m, n, k):
     for i in (4, 5):
         assert np.max(np.abs(a[i] - b[i])) <= 1e-12 * max(1.0, float(np.max(np.abs(b[i]))))
     nb = _nonbasic(n, a[7])
-    assert np.max(np.abs(a[6][nb] - b[6][nb]) / b[6][nb]) <= 1e-12
+    assert np.max(np.abs(a[6][nb] - b[6][nb]) / b[6][nb]) <= 1e-9
