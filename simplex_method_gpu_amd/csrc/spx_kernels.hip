@@ -3973,11 +3973,11 @@ hipError_t launch_generate(double* A, double* b, double* c, int64_t m, int64_t n
 // ---------------------------------------------------------------------------
 // Round 5: both kernels latency-bound no more (C3 steepest pass: the two took
 // about 28 us): k_se_part's threads request a 16-row block of their column at
-// once, and k_se_fin sums the row-block partials of 64 columns per workgroup
-// with 16 slices of threads (coalesced, 16 loads in flight per thread), then
-// the slices in ascending order.
+// once, and k_se_fin sums the row-block partials in slices of threads
+// (coalesced, several loads in flight per thread), then the slices in
+// ascending order.  Round 6: k_ftran_bc forms k_se_part's sums itself on
+// every pass but a window's first (Params::se_fused, 8-row partials).
 constexpr int SE_RB = 16;     // rows per k_se_part workgroup
-constexpr int SE_SLICES = 16;  // k_se_fin: partial slices per column (1024 threads = 64 columns x 16)
 
 // The pending pivot (its alpha parity and the window position): from the
 // state, or -- when the FTRAN pass deferred its tail (TailRec) -- from the
@@ -4043,6 +4043,14 @@ __global__ __launch_bounds__(256) void k_se_part(Params P) {
     }
 }
 
+// (Round 6: SE_FC columns per workgroup and SE_FS slices of partials each --
+// 16 x 64 instead of 64 x 16 -- so the sums of a C3 pass's ~520 columns
+// spread over ~33 workgroups instead of 9: with the fused path's 512
+// partials the 9 were bound by their CUs' load rate)
+constexpr int SE_FC = 16;
+constexpr int SE_FS = 1024 / SE_FC;
+constexpr int SE_FB = 8;  // partials per slice per round trip
+
 __global__ __launch_bounds__(1024) void k_se_fin(Params P) {
     int nw;
     const double* al;
@@ -4052,30 +4060,30 @@ __global__ __launch_bounds__(1024) void k_se_fin(Params P) {
     const int S = P.bc ? P.bc_n[0] : (int)m;
     const int ncols = S + KW + 1;
     const int64_t stride = L + KW + 1;
-    const int tid = threadIdx.x, cl = tid & 63, sl = tid >> 6;  // column in the group, slice
-    const int64_t c = (int64_t)blockIdx.x * 64 + cl;
-    __shared__ double red[SE_SLICES][64];
-    // slice sl sums the partials g = sl, sl + 16, ... (ascending), 16 at a time
+    const int tid = threadIdx.x, cl = tid % SE_FC, sl = tid / SE_FC;  // column in the group, slice
+    const int64_t c = (int64_t)blockIdx.x * SE_FC + cl;
+    __shared__ double red[SE_FS][SE_FC];
+    // slice sl sums the partials g = sl, sl + SE_FS, ... (ascending), SE_FB at a time
     double v = 0.0;
     const int64_t cc = c < ncols ? c : 0;
-    const int gend = (int64_t)blockIdx.x * 64 < ncols ? P.se_parts : 0;  // (groups past the columns: nothing)
-    for (int g0 = sl; g0 < gend; g0 += SE_SLICES * 16) {
-        double t[16];
+    const int gend = (int64_t)blockIdx.x * SE_FC < ncols ? P.se_parts : 0;  // (groups past the columns: nothing)
+    for (int g0 = sl; g0 < gend; g0 += SE_FS * SE_FB) {
+        double t[SE_FB];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int g = g0 + k * SE_SLICES;
+        for (int k = 0; k < SE_FB; ++k) {
+            const int g = g0 + k * SE_FS;
             t[k] = P.se_part[(int64_t)(g < P.se_parts ? g : 0) * stride + cc];
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (g0 + k * SE_SLICES < P.se_parts) v += t[k];
+        for (int k = 0; k < SE_FB; ++k)
+            if (g0 + k * SE_FS < P.se_parts) v += t[k];
     }
     red[sl][cl] = v;
     __syncthreads();
     if (sl == 0 && c < ncols) {
         double w = red[0][cl];
-#pragma unroll
-        for (int k = 1; k < SE_SLICES; ++k) w += red[k][cl];
+#pragma unroll 16
+        for (int k = 1; k < SE_FS; ++k) w += red[k][cl];
         if (c < S) P.se_v[P.bc ? (int64_t)P.rlist[c] : c] = w;
         else if (c < S + KW) P.se_cg[c - S] = w;
         else P.se_cg[KW] = 1.0 + w;
@@ -4116,8 +4124,8 @@ hipError_t launch_se_prep(const Params& P, hipStream_t s, int fused_parts) {
     } else {
         hipLaunchKernelGGL(k_se_part, dim3((unsigned)P.se_parts), dim3(256), 0, s, P);
     }
-    // 64 columns per workgroup (the columns in use, S + KW + 1, are at most L + KW + 1)
-    hipLaunchKernelGGL(k_se_fin, dim3((unsigned)((P.L + P.win + 1 + 63) / 64)), dim3(1024), 0, s, Q);
+    // SE_FC columns per workgroup (the columns in use, S + KW + 1, are at most L + KW + 1)
+    hipLaunchKernelGGL(k_se_fin, dim3((unsigned)((P.L + P.win + 1 + SE_FC - 1) / SE_FC)), dim3(1024), 0, s, Q);
     return hipGetLastError();
 }
 
